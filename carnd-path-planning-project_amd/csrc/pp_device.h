@@ -1,0 +1,296 @@
+// pp_device.h — device-side planner stages (gfx950, FP64 VALU).
+//
+// Each function restates one reference routine (file:line of Fable3/CarND-Path-Planning-Project)
+// in the reference's floating-point evaluation order; the library is built with -ffp-contract=off
+// so no mul+add pair is fused. Only transcendentals (atan2/sin/cos from the ROCm device math
+// library) can differ from glibc by an ulp: parity is within 1e-6 m (measured ~1e-12 m).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pp.h"
+
+namespace ppd {
+
+constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
+constexpr double kEps = 1e-5;                     // src/main.cpp:24
+constexpr int kKP = 17;                           // LDS knot stride (16 knots + 1 pad: bank spread)
+
+// Map geometry (SoA). Arrays [i] or [lane * n + i]. llen[lane*n+i] = |lc[i] - lc[i-1]|
+// (Map::get_lane_length, src/main.cpp:138-142), precomputed on the host with the same formula.
+struct MapV {
+    const double *ref_x, *ref_y, *nx, *ny, *lc_x, *lc_y, *llen;
+    int n;
+};
+
+// Per-scene preparation output of K1 (SoA, workspace).
+struct PrepV {
+    double *pos_x, *pos_y, *angle, *ca_m, *sa_m, *ca_p, *sa_p;
+    double *ego_speed, *ego_d, *ego_vd, *ratio /*[3][S]*/, *in_ts, *in_tt, *l_ts /*[3][S]*/,
+        *l_tt /*[3][S]*/, *score /*[3][S]*/;
+    int32_t *K, *ref_wp, *T, *ego_lane, *open_mask, *lim_mask, *status;
+};
+
+// src/main.cpp:134-137 (idx + size) % size, size_t arithmetic
+__device__ __forceinline__ int wpi(int idx, int n) {
+    if (idx >= 0) return idx < n ? idx : idx % n;
+    if (idx >= -n) return idx + n;
+    return (int)(((uint64_t)(int64_t)idx + (uint64_t)n) % (uint64_t)n);
+}
+__device__ __forceinline__ double lane_offset(int lane) { return 4.0 * (lane + 0.5); }  // :84-88
+__device__ __forceinline__ double s_min(double a, double b) { return (b < a) ? b : a; }  // std::min
+__device__ __forceinline__ double s_max(double a, double b) { return (a < b) ? b : a; }  // std::max
+
+// helpers.h:188-249 distancesq_pt_seg
+__device__ __forceinline__ double distsq_pt_seg(double px, double py, double ax, double ay, double bx,
+                                                double by, double& rnom_o, double& rdenom_o,
+                                                double& snom_o) {
+    rnom_o = 0; rdenom_o = 1; snom_o = 0;
+    if (ax == bx && ay == by) return (ax - bx) * (ax - bx) + (ay - by) * (ay - by);
+    const double rdenom = (ax - bx) * (ax - bx) + (ay - by) * (ay - by);
+    const double pdx = px - ax, dx = bx - ax;
+    const double pdy = py - ay, dy = by - ay;
+    const double rnom = pdx * dx + pdy * dy;
+    rdenom_o = rdenom;
+    const double snom = pdx * dy - pdy * dx;
+    snom_o = snom;
+    if (rnom < -1) { rnom_o = 0; return (px - ax) * (px - ax) + (py - ay) * (py - ay); }
+    if (rnom > rdenom) { rnom_o = rdenom; return (px - bx) * (px - bx) + (py - by) * (py - by); }
+    rnom_o = rnom;
+    return snom * snom / rdenom;
+}
+
+// Map::init_reference_waypoint (src/main.cpp:143-197)
+__device__ inline void init_reference_waypoint(const MapV& m, double x, double y, int& ref_wp,
+                                               double ratio[3]) {
+    const int n = m.n;
+    int closest = 0;
+    double cd;
+    { const double dx = m.ref_x[0] - x, dy = m.ref_y[0] - y; cd = dx * dx + dy * dy; }
+    for (int i = 1; i < n; i++) {
+        const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
+        const double d = dx * dx + dy * dy;
+        if (d < cd) { closest = i; cd = d; }
+    }
+    double rnom, snom, rdenom, d0, d1;
+    {
+        const int a = wpi(closest - 1, n), b = wpi(closest, n), c = wpi(closest + 1, n);
+        d0 = distsq_pt_seg(x, y, m.ref_x[a], m.ref_y[a], m.ref_x[b], m.ref_y[b], rnom, rdenom, snom);
+        d1 = distsq_pt_seg(x, y, m.ref_x[b], m.ref_y[b], m.ref_x[c], m.ref_y[c], rnom, rdenom, snom);
+        if (d1 < d0) {
+            closest++;
+        } else if (d1 == d0) {
+            const double anx = (m.nx[a] + m.nx[b]) / 2, any = (m.ny[a] + m.ny[b]) / 2;
+            const double dpx = x - m.ref_x[b], dpy = y - m.ref_y[b];
+            const double dotp = anx * dpx + any * dpy;
+            if (dotp > 0) closest++;
+        }
+    }
+    ref_wp = closest;
+    const int a = wpi(closest - 1, n), b = wpi(closest, n);
+    for (int lane = 0; lane < 3; lane++) {
+        distsq_pt_seg(x, y, m.lc_x[lane * n + a], m.lc_y[lane * n + a], m.lc_x[lane * n + b],
+                      m.lc_y[lane * n + b], rnom, rdenom, snom);
+        ratio[lane] = rnom / rdenom;
+    }
+}
+
+// Map::lane_matching (src/main.cpp:199-275); bounded walk (never reached on finite input).
+__device__ inline bool lane_matching(const MapV& m, int ref_wp, const double ratio[3], double x,
+                                     double y, double& out_s, double& out_d, int& out_lane,
+                                     int& out_next_wp) {
+    const int n = m.n;
+    int dir = 0;
+    bool stop = false;
+    int cur = ref_wp;
+    double sum_s0 = 0, sum_s1 = 0, sum_s2 = 0;
+    double sr0 = ratio[0], sr1 = ratio[1], sr2 = ratio[2];
+    double best = 1000 * 1000;
+    bool found = false;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        bool improved = false;
+        const int a = wpi(cur - 1, n), b = wpi(cur, n);
+#pragma unroll
+        for (int lane = 0; lane < 3; lane++) {
+            double rnom, snom, rdenom;
+            const double dsq = distsq_pt_seg(x, y, m.lc_x[lane * n + a], m.lc_y[lane * n + a],
+                                             m.lc_x[lane * n + b], m.lc_y[lane * n + b], rnom,
+                                             rdenom, snom);
+            if (dsq < best) {
+                best = dsq;
+                improved = true;
+                found = true;
+                const double sr = lane == 0 ? sr0 : (lane == 1 ? sr1 : sr2);
+                const double ss = lane == 0 ? sum_s0 : (lane == 1 ? sum_s1 : sum_s2);
+                const double rfs = rnom / rdenom;
+                const double r_mod = rfs - sr;
+                const double seg_len = m.llen[lane * n + b];
+                out_s = ss + seg_len * r_mod;
+                double d = sqrt(dsq);
+                if (snom < 0) d = -d;
+                out_d = d + lane_offset(lane);
+                out_lane = lane;
+                out_next_wp = cur;
+            }
+            if (rnom == 0) {
+                if (dir == 1) stop = true;
+                dir = -1;
+            } else if (rnom == rdenom) {
+                if (dir == -1) stop = true;
+                dir = 1;
+            } else {
+                stop = true;
+            }
+        }
+        if (!improved || stop) break;
+        const double l0 = m.llen[0 * n + b], l1 = m.llen[1 * n + b], l2 = m.llen[2 * n + b];
+        if (dir > 0) {
+            sum_s0 += (1 - sr0) * l0; sum_s1 += (1 - sr1) * l1; sum_s2 += (1 - sr2) * l2;
+            sr0 = sr1 = sr2 = 0;
+            cur++;
+        } else {
+            sum_s0 -= sr0 * l0; sum_s1 -= sr1 * l1; sum_s2 -= sr2 * l2;
+            sr0 = sr1 = sr2 = 1;
+            cur--;
+        }
+    }
+    return found;
+}
+
+// Map::project_speed (src/main.cpp:330-358)
+__device__ inline void project_speed(const MapV& m, double vx, double vy, int next_wp, double& vs,
+                                     double& vd) {
+    const int n = m.n;
+    const int a = wpi(next_wp - 1, n), b = wpi(next_wp, n);
+    double wx = m.ref_x[b] - m.ref_x[a], wy = m.ref_y[b] - m.ref_y[a];
+    const double svl = sqrt(vx * vx + vy * vy);
+    if (svl < kEps) {
+        vs = svl;
+        vd = 0;
+        return;
+    }
+    const double wvl = sqrt(wx * wx + wy * wy);
+    wx *= svl / wvl;
+    wy *= svl / wvl;
+    double sign = 1.0;
+    if (wx * vx + wy * vy < 0) { vx *= -1; vy *= -1; sign = -1; }
+    double rnom, rdenom, snom;
+    distsq_pt_seg(vx, vy, 0.0, 0.0, wx, wy, rnom, rdenom, snom);
+    vs = (rnom / rdenom) * svl * sign;
+    vd = (snom / rdenom) * svl * sign;
+}
+
+// Map::get_lane_pos (src/main.cpp:277-328) on one lane. ok=false if the bounded walk ran out.
+__device__ inline void get_lane_pos(const MapV& m, int ref_wp, double ratio, double s, int lane,
+                                    double& ox, double& oy, bool& ok) {
+    const int n = m.n;
+    int wp = ref_wp;
+    double nx_ = 0, ny_ = 0, px_ = 0, py_ = 0, dest = 0;
+    ok = false;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        const int b = wpi(wp, n), a = wpi(wp - 1, n);
+        nx_ = m.lc_x[lane * n + b]; ny_ = m.lc_y[lane * n + b];
+        px_ = m.lc_x[lane * n + a]; py_ = m.lc_y[lane * n + a];
+        const double wl = m.llen[lane * n + b];
+        if (s > 0) {
+            const double rem = wl * (1 - ratio);
+            if (s <= rem) { dest = 1 - (rem - s) / wl; ok = true; break; }
+            s -= rem;
+            ratio = 0;
+            wp++;
+        } else {
+            const double rem = wl * ratio;
+            if (-s <= rem) { dest = (rem + s) / wl; ok = true; break; }
+            s += rem;
+            ratio = 1;
+            wp--;
+        }
+    }
+    ox = nx_ * dest + px_ * (1 - dest);
+    oy = ny_ * dest + py_ * (1 - dest);
+}
+
+// SpeedController (src/main.cpp:488-548)
+struct SC { double start, target, ttime, shift; };
+__device__ __forceinline__ double sc_get_speed(const SC& c, double t) {
+    t -= c.shift;
+    if (t < 0) t = 0;
+    if (t > c.ttime) return c.target;
+    return c.start + (c.target - c.start) * t / c.ttime;
+}
+__device__ __forceinline__ void sc_add_limit(SC& c, double nts, double ntt) {
+    const double tm = s_max(c.ttime, 0.02);
+    const double ntm = s_max(ntt, 0.02);
+    const double cg = (c.target - c.start) / tm;
+    const double ng = (nts - c.start) / ntm;
+    if (ng < cg) { c.target = nts; c.ttime = ntt; }
+}
+__device__ __forceinline__ void sc_override(SC& c, double t, double speed) {
+    if (t > c.ttime) return;
+    if (fabs(c.target - c.start) < kEps) return;
+    const double mt = c.ttime * (speed - c.start) / (c.target - c.start);
+    c.shift = t - mt;
+}
+
+// LimitSpeed::calculate (src/main.cpp:1068-1150). Returns 0 FREEFLOW 1 BRAKE 2 MAXBRAKE 3 ADJUST 4 KEEP.
+__device__ inline int limit_speed(const pp_params& P, double fvx, double fvy, double next_s,
+                                  double ego_s, double ego_speed, double ego_acc, bool in_lane,
+                                  double& ts, double& tt, bool& collision) {
+    int code = 0;
+    bool can_acc = true;
+    ts = P.max_speed;
+    tt = fabs(ego_speed - P.max_speed) / P.relaxed_acc;
+    double fcd = next_s - ego_s - P.car_length;
+    collision = false;
+    if (fcd < 0) { fcd = 0; collision = true; }
+    const double fcs = sqrt(fvx * fvx + fvy * fvy);
+    if (ego_speed > fcs) {
+        double acc = P.relaxed_acc;
+        if (ego_acc < 0) acc = P.min_relaxed_acc_while_braking;
+        const double dv = ego_speed - fcs;
+        const double dt = dv / acc;
+        const double dd = ego_speed * dt - dv / 2 * dt;
+        const double max_dist = fcd - P.safety_distance;
+        if (dd > max_dist) {
+            ts = fcs;
+            tt = max_dist / (ego_speed - dv / 2);
+            if (tt < kEps || dv / tt > P.maximum_acc) { code = 2; tt = dv / P.maximum_acc; }
+            else code = 1;
+            can_acc = false;
+        }
+    }
+    if (can_acc && in_lane) {
+        const double excess = ego_s + P.car_length + P.keep_distance - next_s;
+        const double t_opt = s_min(1.0, fabs(excess) / 1.0);
+        if (ego_s + P.car_length + P.keep_distance > next_s) {
+            ts = fcs - excess / t_opt;
+            tt = t_opt;
+            const double mt = fabs(ts - ego_speed) / P.relaxed_acc;   // maximize_acc :1059-1067
+            if (tt < mt) tt = mt;
+            code = 3;
+        } else if (ego_s + P.car_length + P.keep_distance + P.keep_distance_leeway > next_s) {
+            ts = fcs;
+            tt = 1.0;
+            const double mt = fabs(ts - ego_speed) / P.relaxed_acc;
+            if (tt < mt) tt = mt;
+            code = 4;
+        }
+    }
+    return code;
+}
+
+__device__ __forceinline__ uint32_t limit_flag(int code) {
+    return code == 1 ? PP_ST_BRAKE : code == 2 ? PP_ST_MAXBRAKE : code == 3 ? PP_ST_ADJUST
+         : code == 4 ? PP_ST_KEEP : 0u;
+}
+
+// candidate speed grid: k = 0 -> max_speed, else clamp(ego_speed + offset, 0, max_speed)
+__device__ __forceinline__ double cand_speed(const pp_params& P, double ego_speed, int k) {
+    if (k == 0) return P.max_speed;
+    double v = ego_speed + P.speed_offsets[k - 1];
+    if (v < 0) v = 0;
+    if (v > P.max_speed) v = P.max_speed;
+    return v;
+}
+
+}  // namespace ppd

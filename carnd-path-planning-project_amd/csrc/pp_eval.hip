@@ -1,0 +1,1126 @@
+// pp_eval.hip — MI355X (gfx950) batched trajectory-candidate evaluator + its C-ABI.
+//
+// Pipeline per pp_eval call:
+//   K1 k_prep    one lane per scene, map staged in LDS: ego derivation, Frenet frame, car matching,
+//                LaneChangePlanner, follow cars + LimitSpeed per candidate lane
+//                (src/main.cpp:1254-1438) -> per-scene prep record (SoA workspace).
+//   K2 k_cand    one workgroup = SPB scenes x C candidates. Phase A: one lane per (scene, lane)
+//                builds the control points + tk::spline coefficients into LDS
+//                (TrajectoryBuilder::build setup, src/main.cpp:575-904, spline.h:284-373).
+//                Phase B: one lane per candidate runs the 0.02 s resampling loop with the
+//                accel/curvature limiter (src/main.cpp:905-1041) reading its spline from LDS,
+//                computes the candidate cost, and (reference mode) the winning lane writes
+//                next_x/next_y directly.
+//   K3 k_winner  comfort mode only: per-scene argmin + re-run of the winning candidate.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/pp.h"
+#include "pp_device.h"
+#include "pp_synth.h"
+
+using namespace ppd;
+
+// ------------------------------------------------------------------------------------------------
+// K1: scene preparation
+// ------------------------------------------------------------------------------------------------
+struct MapG { const double* buf; int n; };   // 13 arrays of n: ref_x ref_y nx ny lc_x[3] lc_y[3] llen[3]
+
+__device__ __forceinline__ MapV map_view(const double* b, int n) {
+    MapV m;
+    m.ref_x = b; m.ref_y = b + n; m.nx = b + 2 * n; m.ny = b + 3 * n;
+    m.lc_x = b + 4 * n; m.lc_y = b + 7 * n; m.llen = b + 10 * n; m.n = n;
+    return m;
+}
+
+__global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+                                              pp_scene_info* info) {
+    extern __shared__ __attribute__((aligned(16))) double smap[];
+    const int n = mg.n;
+    for (int i = threadIdx.x; i < 13 * n; i += blockDim.x) smap[i] = mg.buf[i];
+    __syncthreads();
+    const MapV m = map_view(smap, n);
+    const int64_t S = in.n_scenes;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+
+    uint32_t status = 0;
+    // ---- ego derivation (src/main.cpp:1233-1292) ----
+    double ego_x = in.ego_x[s], ego_y = in.ego_y[s];
+    const double yaw = in.ego_yaw_deg[s];
+    double ego_speed = in.ego_speed_mph[s];
+    ego_speed /= 2.237;
+    double ego_acc = 0, esv_x = 0, esv_y = 0, dt0 = 0;
+    int K = 0;
+    double p8x = 0, p8y = 0;
+    if (in.n_prev[s] >= PP_PREV_KEEP) {
+        K = PP_PREV_KEEP;
+        const double p7x = in.prev_x[7 * S + s], p7y = in.prev_y[7 * S + s];
+        p8x = in.prev_x[8 * S + s]; p8y = in.prev_y[8 * S + s];
+        const double p9x = in.prev_x[9 * S + s], p9y = in.prev_y[9 * S + s];
+        const double ax = p8x - p7x, ay = p8y - p7y;
+        const double v2 = sqrt(ax * ax + ay * ay);
+        esv_x = p9x - p8x; esv_y = p9y - p8y;
+        const double v3 = sqrt(esv_x * esv_x + esv_y * esv_y);
+        ego_acc = (v3 - v2) * 50;
+        ego_speed = v3 * 50;
+        esv_x *= 50; esv_y *= 50;
+        ego_x = p9x; ego_y = p9y;
+        dt0 = PP_PREV_KEEP / 50.0;
+    }
+    // ---- Frenet frame + ego matching (src/main.cpp:1299-1320) ----
+    int ref_wp;
+    double ratio[3];
+    init_reference_waypoint(m, ego_x, ego_y, ref_wp, ratio);
+    double ego_s = 0, ego_d = 0;
+    int ego_lane = 0, nwp_unused = 0;
+    if (!lane_matching(m, ref_wp, ratio, ego_x, ego_y, ego_s, ego_d, ego_lane, nwp_unused)) {
+        ego_s = ego_d = 0;
+        ego_lane = 0;
+        status |= PP_ST_EGO_UNMATCHED;
+    }
+    double ego_vs, ego_vd;
+    project_speed(m, esv_x, esv_y, ref_wp, ego_vs, ego_vd);
+    if (ego_acc > P.maximum_acc) ego_acc = P.maximum_acc;
+    if (ego_acc < -P.maximum_acc) ego_acc = -P.maximum_acc;
+
+    // ---- one streaming pass over the cars in ascending id (std::map order) ----
+    // LaneChangePlanner accumulation (src/main.cpp:377-445) and follow-car selection
+    // (src/main.cpp:1388-1410) are order-dependent reductions over the same car sequence.
+    const int T_in = in.prev_target_lane[s];
+    double lane_speed[3] = {P.max_speed, P.max_speed, P.max_speed};
+    double next_s[3] = {1000, 1000, 1000};
+    bool open[3] = {true, true, true};
+    int in_id = -1; double in_s = 0, in_vx = 0, in_vy = 0;
+    int t_id[3] = {-1, -1, -1};
+    double t_s[3] = {0, 0, 0}, t_vx[3] = {0, 0, 0}, t_vy[3] = {0, 0, 0};
+    int nmatched = 0;
+    int ncar = in.n_cars[s];
+    if (ncar > in.car_stride) ncar = in.car_stride;
+    for (int j = 0; j < ncar; j++) {
+        const int64_t ix = (int64_t)j * S + s;
+        const int id = in.car_id[ix];
+        const double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+        double cs, cd;
+        int clane = 0, nwp = 0;
+        if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
+            status |= PP_ST_CAR_UNMATCHED;
+            continue;
+        }
+        double cvs, cvd;
+        project_speed(m, cvx, cvy, nwp, cvs, cvd);
+        nmatched++;
+        // planner (src/main.cpp:379-444)
+        const double sp = cs + cvs * dt0;
+        if (sp > ego_s) {
+            if (sp < next_s[clane]) {
+                next_s[clane] = sp;
+                if (sp - ego_s < 200) {
+                    int speed = (int)cvs;
+                    if (speed > P.max_speed) speed = (int)P.max_speed;
+                    if (sp - ego_s > 100)
+                        speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
+                    lane_speed[clane] = speed;
+                }
+            }
+        }
+        double add = 2;
+        if (T_in == clane) add = 0;
+        const double min_dist = P.car_length + P.safety_distance + add;
+        if (fabs(ego_s - sp) < min_dist) open[clane] = false;
+        if (sp > ego_s && cvs < ego_vs) {
+            const double car_dist = sp - ego_s - P.car_length - P.safety_distance - add;
+            const double sd = ego_vs - cvs;
+            const double dtm = sd / P.relaxed_acc;
+            const double ddist = ego_vs * dtm - sd / 2 * dtm;
+            if (car_dist < ddist) open[clane] = false;
+        }
+        if (sp < ego_s && cvs > ego_vs && sp + 50 > ego_s) {
+            const double car_dist = ego_s - sp - P.car_length - P.safety_distance - add;
+            const double sd = cvs - ego_vs;
+            double dtm = sd / P.relaxed_acc;
+            if (T_in == ego_lane) dtm += 2;
+            const double md = sd * dtm;
+            if (car_dist < md) open[clane] = false;
+        }
+        // follow cars (src/main.cpp:1391-1409); the target-lane choice for every candidate lane
+        const double s0 = cs + cvs * dt0;
+        const double d0 = cd + cvd * dt0;
+        if (s0 > ego_s && fabs(d0 - ego_d) < 3) {
+            if (in_id == -1 || in_s > s0) { in_id = id; in_s = s0; in_vx = cvx; in_vy = cvy; }
+        }
+#pragma unroll
+        for (int L = 0; L < 3; L++) {
+            if (s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3) {
+                if (t_id[L] == -1 || t_s[L] > s0) { t_id[L] = id; t_s[L] = s0; t_vx[L] = cvx; t_vy[L] = cvy; }
+            }
+        }
+    }
+    // scores + argmax (src/main.cpp:447-484)
+    int best_lane = ego_lane;
+    double best_score = 0;
+    double score[3];
+#pragma unroll
+    for (int lane = 0; lane < 3; lane++) {
+        score[lane] = 0;
+        if (lane != ego_lane && !open[lane]) continue;
+        const double speed_score = s_min(lane_speed[lane] / P.max_speed, 1.0);
+        const double distance_score = 1 - fabs((double)(T_in - lane)) / 2;
+        const double free_score = s_min(1.0, next_s[lane] / 100);
+        const double total = speed_score + distance_score / 2 + free_score;
+        score[lane] = total;
+        if (total > best_score) { best_score = total; best_lane = lane; }
+    }
+    int T;
+    if (abs(ego_lane - best_lane) > 1) {
+        const int nl = best_lane > ego_lane ? ego_lane + 1 : ego_lane - 1;
+        T = open[nl] ? nl : ego_lane;
+        status |= PP_ST_JUMP_RULE;
+    } else {
+        T = best_lane;
+    }
+    const int open_mask = (open[0] ? 1 : 0) | (open[1] ? 2 : 0) | (open[2] ? 4 : 0);
+    if (open_mask != 7) status |= PP_ST_LANE_CLOSED;
+    if (T != ego_lane) {                                               // src/main.cpp:1358-1369
+        const double dtl = lane_offset(T);
+        const double diff = fabs(ego_vd * 1.0 + ego_d - dtl);
+        if (diff > 6.0) { T = ego_lane; status |= PP_ST_TOO_FAR; }
+    }
+    // LimitSpeed for the in-lane car and the per-lane target car (src/main.cpp:1411-1438)
+    int lim_mask = 0;
+    bool col;
+    if (in_id >= 0) {
+        double ts, tt;
+        const int code = limit_speed(P, in_vx, in_vy, in_s, ego_s, ego_speed, ego_acc, true, ts, tt, col);
+        status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
+        pv.in_ts[s] = ts; pv.in_tt[s] = tt;
+        lim_mask |= 1;
+    }
+#pragma unroll
+    for (int L = 0; L < 3; L++) {
+        if (t_id[L] >= 0 && t_id[L] != in_id) {
+            double ts, tt;
+            const int code = limit_speed(P, t_vx[L], t_vy[L], t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
+            status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
+            pv.l_ts[L * S + s] = ts; pv.l_tt[L * S + s] = tt;
+            lim_mask |= 2 << L;
+        }
+    }
+    // TrajectoryBuilder::build start pose (src/main.cpp:583-610) + frame rotations (:786-823)
+    double pos_x, pos_y, angle;
+    if (K == 0) {
+        pos_x = ego_x; pos_y = ego_y;
+        angle = yaw * kPi / 180;
+    } else {
+        pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
+        const double vx = pos_x - p8x, vy = pos_y - p8y;
+        if (vx * vx + vy * vy < kEps) angle = yaw * kPi / 180;
+        else angle = atan2(pos_y - p8y, pos_x - p8x);
+    }
+    pv.pos_x[s] = pos_x; pv.pos_y[s] = pos_y; pv.angle[s] = angle;
+    pv.ca_m[s] = cos(-angle); pv.sa_m[s] = sin(-angle);
+    pv.ca_p[s] = cos(angle);  pv.sa_p[s] = sin(angle);
+    pv.ego_speed[s] = ego_speed; pv.ego_d[s] = ego_d; pv.ego_vd[s] = ego_vd;
+#pragma unroll
+    for (int l = 0; l < 3; l++) { pv.ratio[l * S + s] = ratio[l]; pv.score[l * S + s] = score[l]; }
+    pv.K[s] = K; pv.ref_wp[s] = ref_wp; pv.T[s] = T; pv.ego_lane[s] = ego_lane;
+    pv.open_mask[s] = open_mask; pv.lim_mask[s] = lim_mask; pv.status[s] = status;
+    if (info) {
+        pp_scene_info I = {};
+        I.ego_x = ego_x; I.ego_y = ego_y; I.ego_speed = ego_speed; I.ego_acc = ego_acc;
+        I.ego_s = ego_s; I.ego_d = ego_d; I.ego_vs = ego_vs; I.ego_vd = ego_vd;
+        for (int l = 0; l < 3; l++) { I.ref_ratio[l] = ratio[l]; I.lane_score[l] = score[l]; }
+        I.ref_wp = ref_wp; I.ego_lane = ego_lane; I.target_lane = T; I.lane_open_mask = open_mask;
+        I.n_matched_cars = nmatched; I.in_lane_car = in_id;
+        info[s] = I;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase A: control points + spline for one (scene, lane) into an LDS slot
+// ------------------------------------------------------------------------------------------------
+struct Slot {          // pointers into LDS, stride kKP per slot
+    double *X, *Y, *A, *B, *C;
+    int* meta;          // [0] n knots, [1] n control points, [2] first control-point knot, [3] flags
+};
+constexpr int kMetaFallback = 1, kMetaTrunc = 2, kMetaWalkFail = 4;
+
+__device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_batch& in,
+                           const PrepV& pv, int64_t s, int L, Slot sl) {
+    const int64_t S = in.n_scenes;
+    const int K = pv.K[s];
+    const double pos_x = pv.pos_x[s], pos_y = pv.pos_y[s];
+    const double ca = pv.ca_m[s], sa = pv.sa_m[s];
+    const double start = pv.ego_speed[s], ego_d = pv.ego_d[s], ego_vd = pv.ego_vd[s];
+    const int ref_wp = pv.ref_wp[s];
+    const double ratio = pv.ratio[L * S + s];
+    int flags = 0;
+    // lane switch time / first control point distance (src/main.cpp:640-731)
+    double min_cpd = start * 1;
+    min_cpd = s_max(min_cpd, 5.0);
+    const double d_diff = lane_offset(L) - ego_d;
+    const double d_acc = 4;
+    bool slow = false;
+    double lst = 2.0;
+    if ((ego_vd < 0) == (d_diff < 0)) {
+        const double dmax = ego_vd * ego_vd / d_acc / 2;
+        if (dmax > fabs(d_diff)) { slow = true; lst = fabs(ego_vd) / d_acc; }
+    }
+    if (!slow) {
+        double rel = ego_vd;
+        if (d_diff < 0) rel *= -1;
+        const double add = fabs(d_diff);
+        const double peak = sqrt(add * d_acc + rel * rel / 2);
+        lst = (peak * 2 - rel) / d_acc;
+    }
+    double dist = start * lst;
+    if (dist < 10.0) dist = 10.0;
+    if (dist > 50) dist = 50;
+    // knots: previous points [0, K-1) then control points, all in the local frame (:786-831)
+    const int npk = K > 0 ? K - 1 : 0;
+    for (int i = 0; i < npk; i++) {
+        const double tx0 = in.prev_x[(int64_t)i * S + s] - pos_x;
+        const double ty0 = in.prev_y[(int64_t)i * S + s] - pos_y;
+        sl.X[i] = tx0 * ca - ty0 * sa;
+        sl.Y[i] = tx0 * sa + ty0 * ca;
+    }
+    // control points (:638, 744-768): first = start pose, then get_lane_pos steps
+    double lx = pos_x, ly = pos_y, total = 0;
+    sl.X[npk] = (pos_x - pos_x) * ca - (pos_y - pos_y) * sa;
+    sl.Y[npk] = (pos_x - pos_x) * sa + (pos_y - pos_y) * ca;
+    int ncp = 1;
+    double cps = dist;
+    for (int i = 0; i < 5; i++) {
+        double npx, npy;
+        bool ok;
+        get_lane_pos(m, ref_wp, ratio, cps, L, npx, npy, ok);
+        if (!ok) flags |= kMetaWalkFail;
+        total += sqrt((npx - lx) * (npx - lx) + (npy - ly) * (npy - ly));
+        lx = npx; ly = npy;
+        const double tx0 = npx - pos_x, ty0 = npy - pos_y;
+        sl.X[npk + ncp] = tx0 * ca - ty0 * sa;
+        sl.Y[npk + ncp] = tx0 * sa + ty0 * ca;
+        ncp++;
+        if (total > 50 && ncp > 2) break;
+        cps += min_cpd;
+    }
+    int nk = npk + ncp;
+    for (int i = 1; i < nk; i++) {                                      // :833-843
+        if (sl.X[i] <= sl.X[i - 1]) { nk = i; flags |= kMetaTrunc; break; }
+    }
+    const bool fallback = nk < 3 || nk <= npk || fabs(ego_d) > 20;      // :848
+    if (fallback) flags |= kMetaFallback;
+    sl.meta[0] = nk; sl.meta[1] = ncp; sl.meta[2] = npk; sl.meta[3] = flags;
+    if (fallback) return;
+    // tk::spline::set_points (spline.h:284-373): tridiagonal band LU, rows preconditioned,
+    // no pivoting. Forward sweep fuses preconditioning, Gauss step and l_solve row by row
+    // (the reference's values are row-local, so the interleaving is exact);
+    // temporaries: A <- scaled upper band, C <- final diagonal, B <- l_solve result.
+    const int n = nk;
+    double up_prev = 0, dg_prev = 1, yy_prev = 0;
+    for (int i = 0; i < n; i++) {
+        double lo = 0, dg, up = 0, r;
+        if (i == 0) { dg = 2.0; up = 0.0; r = 0.0; }
+        else if (i == n - 1) { dg = 2.0; lo = 0.0; r = 0.0; }
+        else {
+            const double xm = sl.X[i - 1], x0 = sl.X[i], xp = sl.X[i + 1];
+            const double ym = sl.Y[i - 1], y0 = sl.Y[i], yp = sl.Y[i + 1];
+            lo = 1.0 / 3.0 * (x0 - xm);
+            dg = 2.0 / 3.0 * (xp - xm);
+            up = 1.0 / 3.0 * (xp - x0);
+            r = (yp - y0) / (xp - x0) - (y0 - ym) / (x0 - xm);
+        }
+        const double sd = 1.0 / dg;                                     // saved_diag
+        lo *= sd;
+        up *= sd;
+        dg = 1.0;
+        double sum = 0;
+        if (i > 0) {
+            const double xx = -lo / dg_prev;                            // Gauss step k = i-1
+            lo = -xx;
+            dg = dg + xx * up_prev;
+            sum += lo * yy_prev;                                        // l_solve
+        }
+        const double yy = (r * sd) - sum;
+        sl.A[i] = up; sl.C[i] = dg; sl.B[i] = yy;
+        up_prev = up; dg_prev = dg; yy_prev = yy;
+    }
+    double bb_next = 0;
+    for (int i = n - 1; i >= 0; i--) {                                  // r_solve
+        double sum = 0;
+        if (i < n - 1) sum += sl.A[i] * bb_next;
+        const double bb = (sl.B[i] - sum) / sl.C[i];
+        sl.B[i] = bb;
+        bb_next = bb;
+    }
+    for (int i = 0; i < n - 1; i++) {                                   // spline.h:345-349
+        const double dx = sl.X[i + 1] - sl.X[i];
+        sl.A[i] = 1.0 / 3.0 * (sl.B[i + 1] - sl.B[i]) / dx;
+        sl.C[i] = (sl.Y[i + 1] - sl.Y[i]) / dx - 1.0 / 3.0 * (2.0 * sl.B[i] + sl.B[i + 1]) * dx;
+    }
+    const double h = sl.X[n - 1] - sl.X[n - 2];                         // spline.h:367-370
+    sl.A[n - 1] = 0.0;
+    sl.C[n - 1] = 3.0 * sl.A[n - 2] * h * h + 2.0 * sl.B[n - 2] * h + sl.C[n - 2];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase B: the resampling loop of one candidate (src/main.cpp:845-1041)
+// ------------------------------------------------------------------------------------------------
+struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; };
+
+// Output targets: point g (0-based among generated) goes to wx[g*ws], wy[g*ws] (if wx) and
+// px[g*ps], px[g*ps+1] (if px).
+__device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double cy, double angle,
+                                 double ca0, double sa0, SC sc, int room, double* wx, double* wy,
+                                 int64_t ws, double* px, int64_t ps) {
+    CandRes R;
+    R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0;
+    const int nk = sl.meta[0], ncp = sl.meta[1], npk = sl.meta[2], mflags = sl.meta[3];
+    if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
+    if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
+    double pos_x = 0, pos_y = 0;
+    double ca = ca0, sa = sa0, tangle = angle;
+    double cur_t = 0.02;
+    int ng = 0;
+    if (mflags & kMetaFallback) {                                       // :848-901
+        R.flags |= PP_ST_FALLBACK;
+        const double speed = sc_get_speed(sc, cur_t);
+        double cang = 0;
+        int nc = 1;
+        while (ng < room && nc < ncp) {
+            const double dstep = speed / 50;
+            const double ndx = sl.X[npk + nc] - pos_x, ndy = sl.Y[npk + nc] - pos_y;
+            const double cpd = sqrt(ndx * ndx + ndy * ndy);
+            if (cpd < 5) { nc++; continue; }
+            cur_t += 0.02;
+            const double nca = atan2(ndy, ndx);
+            const double adiff = fmod(nca - cang + 3 * kPi, 2 * kPi) - kPi;
+            const double min_radius = s_max(10.0, speed * speed / 4);
+            const double rps = speed / min_radius;
+            const double mas = rps / 50;
+            if (fabs(adiff) > mas) {
+                if (adiff > 0) cang += mas; else cang -= mas;
+            } else {
+                cang += adiff;
+            }
+            pos_x += cos(cang) * dstep;
+            pos_y += sin(cang) * dstep;
+            const double tx = pos_x * ca - pos_y * sa;
+            const double ty = pos_x * sa + pos_y * ca;
+            if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+            if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+            ng++;
+            R.travelled += dstep;
+        }
+        R.ng = ng;
+        return R;
+    }
+    const double x_first = sl.X[0], x_last = sl.X[nk - 1];
+    const double b0 = sl.B[0], c0 = sl.C[0], y0 = sl.Y[0];
+    const double bl = sl.B[nk - 1], cl = sl.C[nk - 1], yl = sl.Y[nk - 1];
+    int cnt = 0;                     // #knots with X < x (std::lower_bound position)
+    double arg = 0, prev_speed = sc.start, prev_angle = 0;
+    while (arg < 50 && ng < room) {
+        double speed = sc_get_speed(sc, cur_t);
+        double dstep = speed / 50;
+        const double x = arg + dstep;
+        // tk::spline::operator() (spline.h:375-396)
+        while (cnt < nk && sl.X[cnt] < x) cnt++;
+        while (cnt > 0 && !(sl.X[cnt - 1] < x)) cnt--;
+        const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+        const double h = x - sl.X[idx];
+        double y;
+        if (x < x_first) y = (b0 * h + c0) * h + y0;
+        else if (x > x_last) y = (bl * h + cl) * h + yl;
+        else y = ((sl.A[idx] * h + sl.B[idx]) * h + sl.C[idx]) * h + sl.Y[idx];
+        const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
+        double acc = fabs(speed - prev_speed) * 50;
+        const double astep = atan2(y - pos_y, x - pos_x);
+        const double adiff = fmod(astep - prev_angle + 3 * kPi, 2 * kPi) - kPi;
+        const double cacc = speed * 50 * fabs(adiff);
+        double eff_c = cacc;
+        if (acc + cacc > P.maximum_acc) {
+            if (speed > prev_speed) {                                   // :945-971
+                double na = P.maximum_acc - cacc;
+                if (na < 0) na = 0;
+                const double ns = prev_speed + na / 50;
+                sc_override(sc, cur_t, ns);
+                speed = ns;
+                sc.ttime += 0.02;
+                dstep = speed / 50;
+                acc = na;
+                R.flags |= PP_ST_ACC_OVERRIDE;
+            }
+            if (acc + cacc > P.maximum_acc) {                           // :972-1018
+                double nc = P.maximum_acc - acc;
+                if (nc < 0) nc = 0;
+                double nad = nc / speed / 50;
+                if (adiff < 0) nad *= -1;
+                const double rot = nad - adiff;
+                double tpx = pos_x * ca - pos_y * sa;
+                double tpy = pos_x * sa + pos_y * ca;
+                tpx = tpx + cx;
+                tpy = tpy + cy;
+                const double vx = cx - tpx, vy = cy - tpy;
+                const double cr = cos(rot), sr = sin(rot);
+                const double rvx = vx * cr - vy * sr;
+                const double rvy = vx * sr + vy * cr;
+                cx = tpx + rvx;
+                cy = tpy + rvy;
+                tangle += rot;
+                ca = cos(tangle);
+                sa = sin(tangle);
+                eff_c = nc;
+                R.flags |= PP_ST_CURV_ADJUST;
+            }
+        }
+        cur_t += 0.02;
+        prev_speed = speed;
+        prev_angle = astep;
+        const double sp_step = (x - pos_x) * dstep / d;
+        pos_y += (y - pos_y) * dstep / d;
+        arg += sp_step;
+        pos_x += sp_step;
+        const double tx = pos_x * ca - pos_y * sa;
+        const double ty = pos_x * sa + pos_y * ca;
+        if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+        if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+        ng++;
+        R.acc_sum += acc + eff_c;
+        R.travelled += dstep;
+    }
+    R.ng = ng;
+    return R;
+}
+
+// per-candidate cost (identical formula in oracle/pp_oracle.c cand_cost)
+__device__ __forceinline__ double cand_cost(const pp_params& P, const CandRes& R, int K, double score_L,
+                                            int L, int T, double v, int open_mask, int ego_lane,
+                                            uint32_t& flags) {
+    const double acc_mean = R.ng > 0 ? R.acc_sum / R.ng : 0.0;
+    const double ideal = (P.n_points - K) * P.max_speed / 50;
+    const double deficit = 1.0 - R.travelled / ideal;
+    double J = (2.5 - score_L) + acc_mean / P.maximum_acc + deficit + ((R.flags & PP_ST_FALLBACK) ? 1.0 : 0.0);
+    if (!(J == J) || (R.flags & PP_ST_NAN)) { J = 999.0; flags |= PP_ST_NAN; }
+    if (J > 999.0) J = 999.0;
+    if (J < 0.0) J = 0.0;
+    if (P.cost_mode == PP_COST_REFERENCE) {
+        if (L != T) J += 1e6;
+        if (v != P.max_speed) J += 1e3;
+    } else {
+        if (!((open_mask >> L) & 1) && L != ego_lane) J += 10.0;
+    }
+    return J;
+}
+
+__device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64_t S, int64_t s,
+                                      int L, double v) {
+    SC sc;                                        // SpeedController ctor (src/main.cpp:495-502)
+    sc.shift = 0;
+    sc.start = pv.ego_speed[s];
+    sc.target = v;
+    sc.ttime = fabs(sc.start - v) / P.relaxed_acc;
+    const int lm = pv.lim_mask[s];
+    if (lm & 1) sc_add_limit(sc, pv.in_ts[s], pv.in_tt[s]);            // :1425-1431
+    if (lm & (2 << L)) sc_add_limit(sc, pv.l_ts[L * S + s], pv.l_tt[L * S + s]);  // :1432-1438
+    return sc;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2: candidates
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+                                              pp_result out, int SPB) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
+    const int nslot = 3 * SPB;
+    double* sX = sm;
+    double* sY = sX + nslot * kKP;
+    double* sA = sY + nslot * kKP;
+    double* sB = sA + nslot * kKP;
+    double* sC = sB + nslot * kKP;
+    int* sMeta = (int*)(sC + nslot * kKP);
+    uint32_t* sFlags = (uint32_t*)(sMeta + 4 * nslot);
+    const MapV m = map_view(mg.buf, mg.n);
+    const int64_t S = in.n_scenes;
+    const int64_t s0 = (int64_t)blockIdx.x * SPB;
+    const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
+    const int tid = threadIdx.x;
+    if (tid < SPB) sFlags[tid] = 0;
+    if (tid < 3 * nsc) {                                               // phase A
+        const int j = tid;
+        Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j};
+        setup_lane(m, P, in, pv, s0 + j / 3, j % 3, sl);
+    }
+    __syncthreads();
+    const int sc_l = tid / C, c = tid - sc_l * C;
+    if (sc_l < nsc) {                                                  // phase B
+        const int64_t s = s0 + sc_l;
+        const int L = c / NS, k = c - L * NS;
+        const int j = sc_l * 3 + L;
+        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j};
+        const double v = cand_speed(P, pv.ego_speed[s], k);
+        const SC sc = make_sc(P, pv, S, s, L, v);
+        const int K = pv.K[s], T = pv.T[s];
+        const bool winner = P.cost_mode == PP_COST_REFERENCE && L == T && k == 0;
+        double* wx = nullptr; double* wy = nullptr;
+        double* px = nullptr;
+        const int64_t ps = (int64_t)C * 2;
+        if (winner) {
+            wx = out.next_x + s * N + K; wy = out.next_y + s * N + K;
+            for (int i = 0; i < K; i++) {
+                out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
+                out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
+            }
+        }
+        if (P.emit_paths && out.paths) {
+            px = out.paths + ((s * N + K) * C + c) * 2;
+            double* p0 = out.paths + ((s * N) * C + c) * 2;
+            for (int i = 0; i < K; i++) {
+                p0[i * ps] = in.prev_x[(int64_t)i * S + s];
+                p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
+            }
+        }
+        const CandRes R = run_candidate(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
+                                        pv.sa_p[s], sc, N - K, wx, wy, 1, px, ps);
+        uint32_t flags = R.flags;
+        const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
+                                      pv.ego_lane[s], flags);
+        out.cost[s * C + c] = cost;
+        if (winner) {
+            for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
+            out.n_out[s] = K + R.ng;
+            out.winner[s] = c;
+        }
+        if (px) {
+            for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
+        }
+        if (P.emit_paths && out.path_len) out.path_len[s * C + c] = K + R.ng;
+        atomicOr(&sFlags[sc_l], flags);
+    }
+    __syncthreads();
+    if (tid < nsc) out.status[s0 + tid] = (uint32_t)pv.status[s0 + tid] | sFlags[tid];
+}
+
+// ------------------------------------------------------------------------------------------------
+// K3: comfort-mode winner (argmin + re-run), one lane per scene, private LDS slot per lane
+// ------------------------------------------------------------------------------------------------
+constexpr int kWinBlock = 64;
+__global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in, pp_params P,
+                                                      PrepV pv, pp_result out) {
+    __shared__ __attribute__((aligned(16))) double wsm[5 * kWinBlock * kKP];
+    __shared__ int wmeta[4 * kWinBlock];
+    const MapV m = map_view(mg.buf, mg.n);
+    const int64_t S = in.n_scenes;
+    const int64_t s = (int64_t)blockIdx.x * kWinBlock + threadIdx.x;
+    if (s >= S) return;
+    const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
+    int best = 0;
+    double bc = out.cost[s * C];
+    for (int c = 1; c < C; c++) {
+        const double v = out.cost[s * C + c];
+        if (v < bc) { bc = v; best = c; }
+    }
+    const int L = best / NS, k = best - L * NS;
+    const int j = threadIdx.x;
+    const Slot sl = {wsm + (0 * kWinBlock + j) * kKP, wsm + (1 * kWinBlock + j) * kKP,
+                     wsm + (2 * kWinBlock + j) * kKP, wsm + (3 * kWinBlock + j) * kKP,
+                     wsm + (4 * kWinBlock + j) * kKP, wmeta + 4 * j};
+    setup_lane(m, P, in, pv, s, L, sl);
+    const double v = cand_speed(P, pv.ego_speed[s], k);
+    const SC sc = make_sc(P, pv, S, s, L, v);
+    const int K = pv.K[s];
+    for (int i = 0; i < K; i++) {
+        out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
+        out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
+    }
+    const CandRes R = run_candidate(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
+                                    pv.sa_p[s], sc, N - K, out.next_x + s * N + K,
+                                    out.next_y + s * N + K, 1, nullptr, 0);
+    for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
+    out.n_out[s] = K + R.ng;
+    out.winner[s] = best;
+}
+
+// ------------------------------------------------------------------------------------------------
+// scene synthesis
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_synth(ppsynth::LaneTables T, uint64_t seed, int64_t first,
+                                               ppsynth::OutBatch o) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= o.S) return;
+    ppsynth::synth_scene(T, seed, first + s, s, o);
+}
+
+// ================================================================================================
+// host side: map, per-device state, C-ABI
+// ================================================================================================
+namespace {
+
+constexpr int kMaxDev = 16;
+constexpr int kPrepD = 7 + 3 + 2 + 3 + 9 + 3;   // doubles per scene in PrepV (see prep_bind)
+constexpr int kPrepI = 7;
+
+struct DevState {
+    bool init = false;
+    double* map = nullptr;        // 13 * n
+    double* lanetab = nullptr;    // synth tables: lc_x[3n] lc_y[3n] seg_len[3n] tan_x[3n] tan_y[3n]
+    void* ws = nullptr;           // prep workspace
+    int64_t ws_cap = 0;
+    void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
+    bool timing = false;          // pp_timing_enable
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<hipEvent_t> ev_rec; // groups of 4: before k_prep, after k_prep, after k_cand, after k_winner
+    std::vector<int> ev_has3;     // per group: k_winner launched
+};
+
+}  // namespace
+
+struct pp_map {
+    int n = 0;
+    std::vector<double> geom;     // 13 * n (MapG layout)
+    std::vector<double> ptab;     // 10 * n: ref xy, normal, 3 lane centers (pp_map_geometry)
+    std::vector<double> lanetab;  // 15 * n
+    DevState dev[kMaxDev];
+    std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d) { if (hipGetDevice(&prev) != hipSuccess) prev = -1; (void)hipSetDevice(d); }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// Map::Init (src/main.cpp:89-131) + derived tables, on the host (done once per map).
+int build_map(pp_map* M, const double* wx, const double* wy, int n) {
+    M->n = n;
+    std::vector<double> nx(n), ny(n), lcx(3 * n), lcy(3 * n);
+    auto W = [n](int i) { return (int)(((int64_t)i + n) % n); };
+    for (int i = 0; i < n; i++) {
+        const int p = W(i - 1);
+        const double dx = wx[i] - wx[p], dy = wy[i] - wy[p];
+        const double len = std::sqrt(dx * dx + dy * dy);
+        if (!(len > 0)) return PP_ERR_ARG;    // duplicate consecutive waypoints: Map::Init divides by 0
+        nx[i] = dy / len;
+        ny[i] = -dx / len;
+    }
+    for (int i = 0; i < n; i++) {
+        const int q = W(i + 1);
+        double ax = (nx[i] + nx[q]) / 2, ay = (ny[i] + ny[q]) / 2;
+        const double a_n = std::atan2(ny[i], nx[i]);
+        const double a_avg = std::atan2(ay, ax);
+        const double cos_alpha = std::cos(a_avg - a_n);
+        ax /= cos_alpha;
+        ay /= cos_alpha;
+        for (int r = 0; r < 3; r++) {
+            const double off = 4.0 * (r + 0.5);
+            lcx[r * n + i] = wx[i] + ax * off;
+            lcy[r * n + i] = wy[i] + ay * off;
+        }
+    }
+    M->geom.assign(13 * (size_t)n, 0.0);
+    double* g = M->geom.data();
+    for (int i = 0; i < n; i++) {
+        g[i] = wx[i]; g[n + i] = wy[i]; g[2 * n + i] = nx[i]; g[3 * n + i] = ny[i];
+        for (int r = 0; r < 3; r++) {
+            g[(4 + r) * n + i] = lcx[r * n + i];
+            g[(7 + r) * n + i] = lcy[r * n + i];
+            const int p = W(i - 1);
+            const double dx = lcx[r * n + i] - lcx[r * n + p], dy = lcy[r * n + i] - lcy[r * n + p];
+            g[(10 + r) * n + i] = std::sqrt(dx * dx + dy * dy);    // Map::get_lane_length
+        }
+    }
+    M->ptab.assign(10 * (size_t)n, 0.0);
+    for (int i = 0; i < n; i++) {
+        double* o = &M->ptab[10 * (size_t)i];
+        o[0] = wx[i]; o[1] = wy[i]; o[2] = nx[i]; o[3] = ny[i];
+        for (int r = 0; r < 3; r++) { o[4 + 2 * r] = lcx[r * n + i]; o[5 + 2 * r] = lcy[r * n + i]; }
+    }
+    M->lanetab.assign(15 * (size_t)n, 0.0);
+    double* t = M->lanetab.data();
+    for (int r = 0; r < 3; r++)
+        for (int i = 0; i < n; i++) {
+            const double len = g[(10 + r) * n + i];
+            const int p = W(i - 1);
+            t[0 * 3 * n + r * n + i] = lcx[r * n + i];
+            t[1 * 3 * n + r * n + i] = lcy[r * n + i];
+            t[2 * 3 * n + r * n + i] = len;
+            t[3 * 3 * n + r * n + i] = (lcx[r * n + i] - lcx[r * n + p]) / len;
+            t[4 * 3 * n + r * n + i] = (lcy[r * n + i] - lcy[r * n + p]) / len;
+        }
+    return PP_OK;
+}
+
+ppsynth::LaneTables lane_tables(const double* t, int n) {
+    ppsynth::LaneTables T;
+    T.n = n; T.lc_x = t; T.lc_y = t + 3 * n; T.seg_len = t + 6 * n; T.tan_x = t + 9 * n; T.tan_y = t + 12 * n;
+    return T;
+}
+
+int dev_init(pp_map* M, int device) {
+    DevState& D = M->dev[device];
+    if (D.init) return PP_OK;
+    if (hipMalloc(&D.map, sizeof(double) * M->geom.size()) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMalloc(&D.lanetab, sizeof(double) * M->lanetab.size()) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMemcpy(D.map, M->geom.data(), sizeof(double) * M->geom.size(), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
+    if (hipMemcpy(D.lanetab, M->lanetab.data(), sizeof(double) * M->lanetab.size(), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
+    D.init = true;
+    return PP_OK;
+}
+
+size_t prep_bytes(int64_t S) { return (size_t)S * (kPrepD * 8 + kPrepI * 4) + 256; }
+
+PrepV prep_bind(void* base, int64_t S) {
+    PrepV p;
+    double* d = (double*)base;
+    double** dd[] = {&p.pos_x, &p.pos_y, &p.angle, &p.ca_m, &p.sa_m, &p.ca_p, &p.sa_p,
+                     &p.ego_speed, &p.ego_d, &p.ego_vd, &p.in_ts, &p.in_tt};
+    int k = 0;
+    for (double** q : dd) *q = d + (int64_t)(k++) * S;
+    p.ratio = d + (int64_t)(k) * S; k += 3;
+    p.l_ts = d + (int64_t)(k) * S; k += 3;
+    p.l_tt = d + (int64_t)(k) * S; k += 3;
+    p.score = d + (int64_t)(k) * S; k += 3;
+    // k == kPrepD
+    int32_t* ip = (int32_t*)(d + (int64_t)kPrepD * S);
+    int32_t** ii[] = {&p.K, &p.ref_wp, &p.T, &p.ego_lane, &p.open_mask, &p.lim_mask, &p.status};
+    int m = 0;
+    for (int32_t** q : ii) *q = ip + (int64_t)(m++) * S;
+    return p;
+}
+
+int ensure_ws(pp_map* M, int device, int64_t S) {
+    DevState& D = M->dev[device];
+    if (D.ws_cap >= S) return PP_OK;
+    if (D.ws) { (void)hipDeviceSynchronize(); (void)hipFree(D.ws); D.ws = nullptr; D.ws_cap = 0; }
+    if (hipMalloc(&D.ws, prep_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
+    D.ws_cap = S;
+    return PP_OK;
+}
+
+int cands_per_block(int C) {
+    int spb = 256 / C;
+    if (spb > 21) spb = 21;      // <= 63 LDS slots per workgroup
+    if (spb < 1) spb = 1;
+    return spb;
+}
+
+bool params_ok(const pp_params* p) {
+    return p && p->n_points > PP_PREV_KEEP && p->n_points <= PP_MAX_POINTS && p->n_speeds >= 1 &&
+           p->n_speeds <= PP_MAX_SPEEDS && 3 * p->n_speeds <= 256 &&
+           (p->cost_mode == PP_COST_REFERENCE || p->cost_mode == PP_COST_COMFORT);
+}
+
+}  // namespace
+
+extern "C" {
+
+void pp_params_default(pp_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->n_points = 50;
+    p->n_speeds = 5;
+    p->cost_mode = PP_COST_REFERENCE;
+    p->emit_paths = 0;
+    const double offs[4] = {-4.0, -2.0, 0.0, 2.0};      // SURVEY.md §8(d) speed grid
+    for (int i = 0; i < 4; i++) p->speed_offsets[i] = offs[i];
+    p->relaxed_acc = 5;                  // src/main.cpp:39-49
+    p->min_relaxed_acc_while_braking = 4;
+    p->maximum_acc = 8;
+    p->max_speed = 22.2;
+    p->car_length = 4.5;
+    p->safety_distance = 2;
+    p->keep_distance = 10;
+    p->keep_distance_leeway = 0.5;
+}
+
+int32_t pp_num_candidates(const pp_params* p) { return p ? 3 * p->n_speeds : 0; }
+
+const char* pp_version(void) { return "pp-mi355x 0.1 (gfx950, fp64, lane-per-candidate)"; }
+
+int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out) {
+    if (!wx || !wy || !out || n < 3 || n > 600) return PP_ERR_ARG;   // map staged in LDS: 13 * n doubles <= 64 KB
+    pp_map* M = new (std::nothrow) pp_map();
+    if (!M) return PP_ERR_NOMEM;
+    const int rc = build_map(M, wx, wy, n);
+    if (rc != PP_OK) { delete M; return rc; }
+    *out = M;
+    return PP_OK;
+}
+
+int32_t pp_map_destroy(pp_map* M) {
+    if (!M) return PP_ERR_ARG;
+    for (int d = 0; d < kMaxDev; d++) {
+        DevState& D = M->dev[d];
+        if (!D.init) continue;
+        DeviceGuard g(d);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(D.map); (void)hipFree(D.lanetab);
+        if (D.ws) (void)hipFree(D.ws);
+        if (D.frame) (void)hipFree(D.frame);
+        for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
+        for (hipEvent_t e : D.ev_rec) (void)hipEventDestroy(e);
+    }
+    delete M;
+    return PP_OK;
+}
+
+int32_t pp_map_geometry(const pp_map* M, double* out10, int32_t n) {
+    if (!M || !out10 || n != M->n) return PP_ERR_ARG;
+    memcpy(out10, M->ptab.data(), sizeof(double) * 10 * (size_t)n);
+    return PP_OK;
+}
+
+int32_t pp_reserve(pp_map* M, int32_t device, int64_t max_scenes) {
+    if (!M || device < 0 || device >= kMaxDev || max_scenes < 0) return PP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(M->mu);
+    DeviceGuard g(device);
+    int rc = dev_init(M, device);
+    if (rc) return rc;
+    return ensure_ws(M, device, max_scenes);
+}
+
+int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
+                int32_t device, void* hip_stream) {
+    if (!M || !in || !out || !params_ok(prm) || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
+    if (in->n_scenes < 0 || in->car_stride < 0 || in->car_stride > PP_MAX_CARS) return PP_ERR_ARG;
+    if (in->n_scenes == 0) return PP_OK;
+    if (!in->ego_x || !in->ego_y || !in->ego_yaw_deg || !in->ego_speed_mph || !in->prev_x ||
+        !in->prev_y || !in->n_prev || !in->prev_target_lane || !in->n_cars ||
+        (in->car_stride > 0 && (!in->car_id || !in->car_x || !in->car_y || !in->car_vx || !in->car_vy)))
+        return PP_ERR_ARG;
+    if (!out->winner || !out->n_out || !out->next_x || !out->next_y || !out->cost || !out->status)
+        return PP_ERR_ARG;
+    if (prm->emit_paths && !out->paths) return PP_ERR_ARG;
+    DeviceGuard g(device);
+    hipStream_t st = (hipStream_t)hip_stream;
+    const int64_t S = in->n_scenes;
+    PrepV pv;
+    MapG mg;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        int rc = dev_init(M, device);
+        if (rc) return rc;
+        rc = ensure_ws(M, device, S);
+        if (rc) return rc;
+        pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
+        mg.buf = M->dev[device].map;
+        mg.n = M->n;
+    }
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool timing = false;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        DevState& D = M->dev[device];
+        if (D.timing) {
+            timing = true;
+            for (int i = 0; i < 4; i++) {
+                if (D.ev_pool.empty()) {
+                    hipEvent_t e;
+                    if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
+                    D.ev_pool.push_back(e);
+                }
+                ev[i] = D.ev_pool.back();
+                D.ev_pool.pop_back();
+                D.ev_rec.push_back(ev[i]);
+            }
+            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT ? 1 : 0);
+        }
+    }
+    pp_params P = *prm;
+    pp_scene_batch B = *in;
+    pp_result R = *out;
+    if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
+    // K1
+    {
+        const int threads = 256;
+        const int64_t blocks = (S + threads - 1) / threads;
+        const size_t lds = sizeof(double) * 13 * (size_t)mg.n;
+        if (timing) (void)hipEventRecord(ev[0], st);
+        hipLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info);
+    }
+    // K2
+    {
+        const int C = 3 * P.n_speeds;
+        const int spb = cands_per_block(C);
+        const int threads = ((spb * C + 63) / 64) * 64;
+        const int nslot = 3 * spb;
+        const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
+        const int64_t blocks = (S + spb - 1) / spb;
+        if (timing) (void)hipEventRecord(ev[1], st);
+        hipLaunchKernelGGL(k_cand, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+    }
+    if (timing) (void)hipEventRecord(ev[2], st);
+    // K3 (comfort mode)
+    if (P.cost_mode == PP_COST_COMFORT) {
+        const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
+        hipLaunchKernelGGL(k_winner, dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+    }
+    if (timing) (void)hipEventRecord(ev[3], st);
+    if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+    return PP_OK;
+}
+
+int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
+    if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(M->mu);
+    M->dev[device].timing = enable != 0;
+    return PP_OK;
+}
+
+int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches3) {
+    if (!M || device < 0 || device >= kMaxDev || !ms3 || !launches3) return PP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(M->mu);
+    DevState& D = M->dev[device];
+    DeviceGuard g(device);
+    for (int k = 0; k < 3; k++) { ms3[k] = 0; launches3[k] = 0; }
+    int rc = PP_OK;
+    const size_t ng = D.ev_rec.size() / 4;
+    for (size_t i = 0; i < ng; i++) {
+        hipEvent_t* e = &D.ev_rec[4 * i];
+        if (hipEventSynchronize(e[3]) != hipSuccess) rc = PP_ERR_HIP;
+        float t;
+        if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
+        if (hipEventElapsedTime(&t, e[1], e[2]) == hipSuccess) { ms3[1] += t; launches3[1]++; } else rc = PP_ERR_HIP;
+        if (D.ev_has3[i]) {
+            if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
+        }
+        for (int k = 0; k < 4; k++) D.ev_pool.push_back(e[k]);
+    }
+    D.ev_rec.clear();
+    D.ev_has3.clear();
+    return rc;
+}
+
+int32_t pp_synth_scenes(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* out,
+                        int32_t device, void* hip_stream) {
+    if (!M || !out || device < 0 || device >= kMaxDev || out->n_scenes < 0 || first_scene < 0) return PP_ERR_ARG;
+    if (out->car_stride < ppsynth::kSynthCars) return PP_ERR_ARG;
+    if (out->n_scenes == 0) return PP_OK;
+    DeviceGuard g(device);
+    ppsynth::LaneTables T;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        const int rc = dev_init(M, device);
+        if (rc) return rc;
+        T = lane_tables(M->dev[device].lanetab, M->n);
+    }
+    ppsynth::OutBatch o;
+    o.S = out->n_scenes;
+    o.ego_x = (double*)out->ego_x; o.ego_y = (double*)out->ego_y;
+    o.ego_yaw_deg = (double*)out->ego_yaw_deg; o.ego_speed_mph = (double*)out->ego_speed_mph;
+    o.prev_x = (double*)out->prev_x; o.prev_y = (double*)out->prev_y;
+    o.n_prev = (int32_t*)out->n_prev; o.prev_target_lane = (int32_t*)out->prev_target_lane;
+    o.n_cars = (int32_t*)out->n_cars; o.car_id = (int32_t*)out->car_id;
+    o.car_x = (double*)out->car_x; o.car_y = (double*)out->car_y;
+    o.car_vx = (double*)out->car_vx; o.car_vy = (double*)out->car_vy;
+    const int threads = 256;
+    const int64_t blocks = (o.S + threads - 1) / threads;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)hip_stream, T, seed, first_scene, o);
+    if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+    return PP_OK;
+}
+
+int32_t pp_synth_scenes_host(const pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* out) {
+    if (!M || !out || out->n_scenes < 0 || first_scene < 0 || out->car_stride < ppsynth::kSynthCars) return PP_ERR_ARG;
+    const ppsynth::LaneTables T = lane_tables(M->lanetab.data(), M->n);
+    ppsynth::OutBatch o;
+    o.S = out->n_scenes;
+    o.ego_x = (double*)out->ego_x; o.ego_y = (double*)out->ego_y;
+    o.ego_yaw_deg = (double*)out->ego_yaw_deg; o.ego_speed_mph = (double*)out->ego_speed_mph;
+    o.prev_x = (double*)out->prev_x; o.prev_y = (double*)out->prev_y;
+    o.n_prev = (int32_t*)out->n_prev; o.prev_target_lane = (int32_t*)out->prev_target_lane;
+    o.n_cars = (int32_t*)out->n_cars; o.car_id = (int32_t*)out->car_id;
+    o.car_x = (double*)out->car_x; o.car_y = (double*)out->car_y;
+    o.car_vx = (double*)out->car_vx; o.car_vy = (double*)out->car_vy;
+    for (int64_t s = 0; s < o.S; s++) ppsynth::synth_scene(T, seed, first_scene + s, s, o);
+    return PP_OK;
+}
+
+// One telemetry frame (the onMessage replacement): C = 3 (one speed: max_speed), reference mode.
+int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, double ego_yaw_deg,
+                      double ego_speed_mph, const double* prev_x, const double* prev_y, int32_t n_prev,
+                      const int32_t* car_id, const double* car_x, const double* car_y,
+                      const double* car_vx, const double* car_vy, int32_t n_cars,
+                      int32_t* target_lane, double* next_x, double* next_y, int32_t* n_out) {
+    if (!M || !target_lane || !next_x || !next_y || !n_out || n_cars < 0 || n_cars > PP_MAX_CARS ||
+        device < 0 || device >= kMaxDev || (n_prev > 0 && (!prev_x || !prev_y)) ||
+        (n_cars > 0 && (!car_id || !car_x || !car_y || !car_vx || !car_vy)))
+        return PP_ERR_ARG;
+    if (*target_lane < 0 || *target_lane > 2) return PP_ERR_ARG;
+    // host staging: one scene, SoA with S = 1 (std::map order: stable sort by id, last row of a
+    // duplicated id wins as in `sensor_fusion_cars[id]` assignment, src/main.cpp:1329)
+    struct Row { int32_t id; double x, y, vx, vy; };
+    std::vector<Row> rows;
+    for (int j = 0; j < n_cars; j++) {
+        bool dup = false;
+        for (auto& r : rows) if (r.id == car_id[j]) { r = {car_id[j], car_x[j], car_y[j], car_vx[j], car_vy[j]}; dup = true; }
+        if (!dup) rows.push_back({car_id[j], car_x[j], car_y[j], car_vx[j], car_vy[j]});
+    }
+    std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.id < b.id; });
+    const int nc = (int)rows.size();
+    // device scratch layout (bytes): doubles then ints
+    constexpr int N = 50;
+    struct Frame {
+        double ego[4], px[PP_PREV_KEEP], py[PP_PREV_KEEP], cx[PP_MAX_CARS], cy[PP_MAX_CARS],
+            cvx[PP_MAX_CARS], cvy[PP_MAX_CARS];
+        double nx[N], ny[N], cost[3];
+        int32_t nprev, ptl, ncars, cid[PP_MAX_CARS], winner, nout;
+        uint32_t status;
+    };
+    Frame h;
+    memset(&h, 0, sizeof(h));
+    h.ego[0] = ego_x; h.ego[1] = ego_y; h.ego[2] = ego_yaw_deg; h.ego[3] = ego_speed_mph;
+    for (int i = 0; i < PP_PREV_KEEP && i < n_prev; i++) { h.px[i] = prev_x[i]; h.py[i] = prev_y[i]; }
+    h.nprev = n_prev; h.ptl = *target_lane; h.ncars = nc;
+    for (int j = 0; j < nc; j++) {
+        h.cid[j] = rows[j].id; h.cx[j] = rows[j].x; h.cy[j] = rows[j].y; h.cvx[j] = rows[j].vx; h.cvy[j] = rows[j].vy;
+    }
+    DeviceGuard g(device);
+    Frame* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        int rc = dev_init(M, device);
+        if (rc) return rc;
+        if (!M->dev[device].frame && hipMalloc(&M->dev[device].frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
+        d = (Frame*)M->dev[device].frame;
+    }
+    if (hipMemcpy(d, &h, sizeof(Frame), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
+    pp_scene_batch B;
+    memset(&B, 0, sizeof(B));
+    B.n_scenes = 1; B.car_stride = PP_MAX_CARS;
+    B.ego_x = &d->ego[0]; B.ego_y = &d->ego[1]; B.ego_yaw_deg = &d->ego[2]; B.ego_speed_mph = &d->ego[3];
+    B.prev_x = d->px; B.prev_y = d->py; B.n_prev = &d->nprev; B.prev_target_lane = &d->ptl;
+    B.n_cars = &d->ncars; B.car_id = d->cid; B.car_x = d->cx; B.car_y = d->cy; B.car_vx = d->cvx; B.car_vy = d->cvy;
+    pp_params P;
+    pp_params_default(&P);
+    P.n_speeds = 1;
+    pp_scene_info* dinfo = nullptr;
+    if (hipMalloc(&dinfo, sizeof(pp_scene_info)) != hipSuccess) return PP_ERR_NOMEM;
+    pp_result R;
+    memset(&R, 0, sizeof(R));
+    R.winner = &d->winner; R.n_out = &d->nout; R.next_x = d->nx; R.next_y = d->ny; R.cost = d->cost;
+    R.status = &d->status; R.info = dinfo;
+    int rc = pp_eval(M, &B, &P, &R, device, nullptr);
+    if (rc == PP_OK && hipDeviceSynchronize() != hipSuccess) rc = PP_ERR_HIP;
+    pp_scene_info hi;
+    if (rc == PP_OK && hipMemcpy(&h, d, sizeof(Frame), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
+    if (rc == PP_OK && hipMemcpy(&hi, dinfo, sizeof(hi), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
+    (void)hipFree(dinfo);
+    if (rc != PP_OK) return rc;
+    *n_out = h.nout;
+    for (int i = 0; i < h.nout && i < N; i++) { next_x[i] = h.nx[i]; next_y[i] = h.ny[i]; }
+    *target_lane = hi.target_lane;
+    return PP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,346 @@
+"""ppamd — Python bindings (ctypes) over the C-ABI in include/pp.h.
+
+The compute path is the HIP library ``libppamd.so`` built for gfx950 from ``csrc/``; this module
+only marshals buffers. Importing it fails loudly if the library is missing: there is no CPU
+fallback for the planner (the CPU restatement under ``oracle/`` is test infrastructure only).
+
+Reference interface mirrored: the per-frame ``onMessage`` compute body of
+Fable3/CarND-Path-Planning-Project ``src/main.cpp:1229-1457`` (see ``plan_frame``) and, batched,
+``TrajectoryBuilder::build`` over a (lane, target speed) candidate grid (see ``evaluate``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libppamd.so")
+
+NUM_LANES = 3
+PREV_KEEP = 10
+MAX_CARS = 16
+MAX_SPEEDS = 8
+MAX_POINTS = 128
+
+COST_REFERENCE = 0
+COST_COMFORT = 1
+
+STATUS_BITS = {
+    "EGO_UNMATCHED": 1 << 0, "CAR_UNMATCHED": 1 << 1, "FALLBACK": 1 << 2, "SPLINE_TRUNC": 1 << 3,
+    "NAN": 1 << 4, "COLLISION": 1 << 5, "ACC_OVERRIDE": 1 << 6, "CURV_ADJUST": 1 << 7,
+    "TOO_FAR": 1 << 8, "BRAKE": 1 << 9, "MAXBRAKE": 1 << 10, "ADJUST": 1 << 11, "KEEP": 1 << 12,
+    "LANE_CLOSED": 1 << 13, "JUMP_RULE": 1 << 14,
+}
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+_up = C.POINTER(C.c_uint32)
+
+
+class SceneBatch(C.Structure):
+    _fields_ = [("n_scenes", C.c_int64), ("car_stride", C.c_int32), ("_pad", C.c_int32),
+                ("ego_x", C.c_void_p), ("ego_y", C.c_void_p), ("ego_yaw_deg", C.c_void_p),
+                ("ego_speed_mph", C.c_void_p), ("prev_x", C.c_void_p), ("prev_y", C.c_void_p),
+                ("n_prev", C.c_void_p), ("prev_target_lane", C.c_void_p), ("n_cars", C.c_void_p),
+                ("car_id", C.c_void_p), ("car_x", C.c_void_p), ("car_y", C.c_void_p),
+                ("car_vx", C.c_void_p), ("car_vy", C.c_void_p)]
+
+
+class Params(C.Structure):
+    _fields_ = [("n_points", C.c_int32), ("n_speeds", C.c_int32), ("cost_mode", C.c_int32),
+                ("emit_paths", C.c_int32), ("speed_offsets", C.c_double * MAX_SPEEDS),
+                ("relaxed_acc", C.c_double), ("min_relaxed_acc_while_braking", C.c_double),
+                ("maximum_acc", C.c_double), ("max_speed", C.c_double), ("car_length", C.c_double),
+                ("safety_distance", C.c_double), ("keep_distance", C.c_double),
+                ("keep_distance_leeway", C.c_double)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("ego_x", C.c_double), ("ego_y", C.c_double), ("ego_speed", C.c_double),
+                ("ego_acc", C.c_double), ("ego_s", C.c_double), ("ego_d", C.c_double),
+                ("ego_vs", C.c_double), ("ego_vd", C.c_double), ("ref_ratio", C.c_double * 3),
+                ("lane_score", C.c_double * 3), ("ref_wp", C.c_int32), ("ego_lane", C.c_int32),
+                ("target_lane", C.c_int32), ("lane_open_mask", C.c_int32),
+                ("n_matched_cars", C.c_int32), ("in_lane_car", C.c_int32), ("_pad", C.c_int32 * 2)]
+
+
+INFO_DTYPE = np.dtype([("ego_x", "f8"), ("ego_y", "f8"), ("ego_speed", "f8"), ("ego_acc", "f8"),
+                       ("ego_s", "f8"), ("ego_d", "f8"), ("ego_vs", "f8"), ("ego_vd", "f8"),
+                       ("ref_ratio", "f8", 3), ("lane_score", "f8", 3), ("ref_wp", "i4"),
+                       ("ego_lane", "i4"), ("target_lane", "i4"), ("lane_open_mask", "i4"),
+                       ("n_matched_cars", "i4"), ("in_lane_car", "i4"), ("_pad", "i4", 2)])
+assert INFO_DTYPE.itemsize == C.sizeof(SceneInfo)
+
+
+class Result(C.Structure):
+    _fields_ = [("winner", C.c_void_p), ("n_out", C.c_void_p), ("next_x", C.c_void_p),
+                ("next_y", C.c_void_p), ("cost", C.c_void_p), ("status", C.c_void_p),
+                ("paths", C.c_void_p), ("path_len", C.c_void_p), ("info", C.c_void_p)]
+
+
+# exported symbols of include/pp.h (checked by tests/test_capi.py)
+EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_create",
+           "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
+           "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read"]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"ppamd: HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    lib.pp_params_default.argtypes = [C.POINTER(Params)]
+    lib.pp_params_default.restype = None
+    lib.pp_num_candidates.argtypes = [C.POINTER(Params)]
+    lib.pp_num_candidates.restype = C.c_int32
+    lib.pp_version.restype = C.c_char_p
+    lib.pp_map_create.argtypes = [_dp, _dp, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.pp_map_create.restype = C.c_int32
+    lib.pp_map_destroy.argtypes = [C.c_void_p]
+    lib.pp_map_destroy.restype = C.c_int32
+    lib.pp_map_geometry.argtypes = [C.c_void_p, _dp, C.c_int32]
+    lib.pp_map_geometry.restype = C.c_int32
+    lib.pp_reserve.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
+    lib.pp_reserve.restype = C.c_int32
+    lib.pp_eval.argtypes = [C.c_void_p, C.POINTER(SceneBatch), C.POINTER(Params),
+                            C.POINTER(Result), C.c_int32, C.c_void_p]
+    lib.pp_eval.restype = C.c_int32
+    lib.pp_synth_scenes.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, C.POINTER(SceneBatch),
+                                    C.c_int32, C.c_void_p]
+    lib.pp_synth_scenes.restype = C.c_int32
+    lib.pp_synth_scenes_host.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, C.POINTER(SceneBatch)]
+    lib.pp_synth_scenes_host.restype = C.c_int32
+    lib.pp_plan_frame.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_double,
+                                  C.c_double, _dp, _dp, C.c_int32, _ip, _dp, _dp, _dp, _dp,
+                                  C.c_int32, _ip, _dp, _dp, _ip]
+    lib.pp_plan_frame.restype = C.c_int32
+    lib.pp_timing_enable.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+    lib.pp_timing_enable.restype = C.c_int32
+    lib.pp_timing_read.argtypes = [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64)]
+    lib.pp_timing_read.restype = C.c_int32
+    return lib
+
+
+lib = _load()
+
+
+class PPError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise PPError(f"{what} failed with status {rc}")
+
+
+def default_params(n_speeds=5, n_points=50, cost_mode=COST_REFERENCE, emit_paths=False,
+                   speed_offsets=None) -> Params:
+    p = Params()
+    lib.pp_params_default(C.byref(p))
+    p.n_speeds = n_speeds
+    p.n_points = n_points
+    p.cost_mode = cost_mode
+    p.emit_paths = 1 if emit_paths else 0
+    if speed_offsets is not None:
+        for i, v in enumerate(speed_offsets):
+            p.speed_offsets[i] = float(v)
+    return p
+
+
+def _ptr(a):
+    """Data pointer of a numpy array or torch tensor (contiguous)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data
+    assert a.is_contiguous()
+    return a.data_ptr()
+
+
+class Map:
+    """Map::Init (src/main.cpp:89-131) over waypoint x/y; lane geometry uploaded per device."""
+
+    def __init__(self, wx, wy):
+        self.wx = np.ascontiguousarray(wx, dtype=np.float64)
+        self.wy = np.ascontiguousarray(wy, dtype=np.float64)
+        self.n = len(self.wx)
+        h = C.c_void_p()
+        _check(lib.pp_map_create(self.wx.ctypes.data_as(_dp), self.wy.ctypes.data_as(_dp),
+                                 self.n, C.byref(h)), "pp_map_create")
+        self.handle = h
+
+    def geometry(self) -> np.ndarray:
+        out = np.zeros((self.n, 10), np.float64)
+        _check(lib.pp_map_geometry(self.handle, out.ctypes.data_as(_dp), self.n), "pp_map_geometry")
+        return out
+
+    def reserve(self, device, max_scenes):
+        _check(lib.pp_reserve(self.handle, device, max_scenes), "pp_reserve")
+
+    def timing(self, device, enable=True):
+        _check(lib.pp_timing_enable(self.handle, device, 1 if enable else 0), "pp_timing_enable")
+
+    def read_timing(self, device):
+        """(ms per kernel [k_prep, k_cand, k_winner], launches per kernel); clears the record."""
+        ms = (C.c_double * 3)()
+        n = (C.c_int64 * 3)()
+        _check(lib.pp_timing_read(self.handle, device, ms, n), "pp_timing_read")
+        return list(ms), list(n)
+
+    def close(self):
+        if self.handle:
+            lib.pp_map_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+SCENE_FIELDS_F = ["ego_x", "ego_y", "ego_yaw_deg", "ego_speed_mph"]
+SCENE_FIELDS_I = ["n_prev", "prev_target_lane", "n_cars"]
+CAR_FIELDS_F = ["car_x", "car_y", "car_vx", "car_vy"]
+
+
+def alloc_scenes(S, car_stride=12, xp="numpy", device=None):
+    """SoA scene arrays (numpy on host, or torch on `device`)."""
+    if xp == "numpy":
+        zf = lambda *sh: np.zeros(sh, np.float64)
+        zi = lambda *sh: np.zeros(sh, np.int32)
+    else:
+        import torch
+        zf = lambda *sh: torch.zeros(sh, dtype=torch.float64, device=device)
+        zi = lambda *sh: torch.zeros(sh, dtype=torch.int32, device=device)
+    d = {k: zf(S) for k in SCENE_FIELDS_F}
+    d.update({k: zi(S) for k in SCENE_FIELDS_I})
+    d["prev_x"] = zf(PREV_KEEP, S)
+    d["prev_y"] = zf(PREV_KEEP, S)
+    d["car_id"] = zi(car_stride, S)
+    d.update({k: zf(car_stride, S) for k in CAR_FIELDS_F})
+    return d
+
+
+def scene_struct(d) -> SceneBatch:
+    b = SceneBatch()
+    b.n_scenes = int(d["ego_x"].shape[0])
+    b.car_stride = int(d["car_id"].shape[0])
+    for k in SCENE_FIELDS_F + SCENE_FIELDS_I + CAR_FIELDS_F + ["prev_x", "prev_y", "car_id"]:
+        setattr(b, k, _ptr(d[k]))
+    return b
+
+
+def scenes_to_numpy(d):
+    return {k: (v if isinstance(v, np.ndarray) else v.cpu().numpy()) for k, v in d.items()}
+
+
+def synth_host(m: Map, S, seed=0x5EED0001, first=0, car_stride=12):
+    d = alloc_scenes(S, car_stride)
+    b = scene_struct(d)
+    _check(lib.pp_synth_scenes_host(m.handle, seed, first, C.byref(b)), "pp_synth_scenes_host")
+    return d
+
+
+def synth_device(m: Map, S, seed=0x5EED0001, first=0, device=0, stream=None, car_stride=12):
+    import torch
+    d = alloc_scenes(S, car_stride, xp="torch", device=torch.device("cuda", device))
+    b = scene_struct(d)
+    _check(lib.pp_synth_scenes(m.handle, seed, first, C.byref(b), device, stream), "pp_synth_scenes")
+    return d
+
+
+def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
+    Cn = 3 * prm.n_speeds
+    N = prm.n_points
+    if xp == "numpy":
+        mk = lambda sh, dt: np.zeros(sh, dt)
+        f8, i4, u4 = np.float64, np.int32, np.uint32
+    else:
+        import torch
+        mk = lambda sh, dt: torch.zeros(sh, dtype=dt, device=device)
+        f8, i4, u4 = torch.float64, torch.int32, torch.int32
+    r = {"winner": mk((S,), i4), "n_out": mk((S,), i4), "next_x": mk((S, N), f8),
+         "next_y": mk((S, N), f8), "cost": mk((S, Cn), f8), "status": mk((S,), u4)}
+    if prm.emit_paths:
+        r["paths"] = mk((S, N, Cn, 2), f8)
+        r["path_len"] = mk((S, Cn), i4)
+    if info:
+        if xp == "numpy":
+            r["info"] = np.zeros((S,), INFO_DTYPE)
+        else:
+            import torch
+            r["info"] = torch.zeros((S, INFO_DTYPE.itemsize), dtype=torch.uint8, device=device)
+    return r
+
+
+def result_struct(r) -> Result:
+    R = Result()
+    for k in ["winner", "n_out", "next_x", "next_y", "cost", "status", "paths", "path_len", "info"]:
+        setattr(R, k, _ptr(r.get(k)))
+    return R
+
+
+def result_to_numpy(r):
+    out = {}
+    for k, v in r.items():
+        a = v if isinstance(v, np.ndarray) else v.cpu().numpy()
+        if k == "status":
+            a = a.view(np.uint32)
+        if k == "info" and a.dtype == np.uint8:
+            a = a.view(INFO_DTYPE).reshape(-1)
+        out[k] = a
+    return out
+
+
+def evaluate(m: Map, scenes, prm: Params, result, device=0, stream=None):
+    """pp_eval over device-resident scene/result buffers (torch tensors on cuda:device)."""
+    b = scene_struct(scenes)
+    R = result_struct(result)
+    _check(lib.pp_eval(m.handle, C.byref(b), C.byref(prm), C.byref(R), device, stream), "pp_eval")
+
+
+def plan_frame(m: Map, ego_x, ego_y, ego_yaw_deg, ego_speed_mph, prev_x, prev_y, cars,
+               target_lane=1, device=0):
+    """The onMessage replacement (src/main.cpp:1229-1466) for one telemetry frame.
+
+    cars: iterable of (id, x, y, vx, vy[, s, d]) rows, as in the simulator's sensor_fusion.
+    Returns (next_x, next_y, new_target_lane).
+    """
+    px = np.ascontiguousarray(prev_x, np.float64)
+    py = np.ascontiguousarray(prev_y, np.float64)
+    rows = [tuple(r)[:5] for r in cars]
+    ids = np.array([int(r[0]) for r in rows], np.int32)
+    cx = np.array([r[1] for r in rows], np.float64)
+    cy = np.array([r[2] for r in rows], np.float64)
+    cvx = np.array([r[3] for r in rows], np.float64)
+    cvy = np.array([r[4] for r in rows], np.float64)
+    tl = C.c_int32(target_lane)
+    nx = np.zeros(50, np.float64)
+    ny = np.zeros(50, np.float64)
+    n_out = C.c_int32(0)
+    _check(lib.pp_plan_frame(m.handle, device, ego_x, ego_y, ego_yaw_deg, ego_speed_mph,
+                             px.ctypes.data_as(_dp), py.ctypes.data_as(_dp), len(px),
+                             ids.ctypes.data_as(_ip), cx.ctypes.data_as(_dp),
+                             cy.ctypes.data_as(_dp), cvx.ctypes.data_as(_dp),
+                             cvy.ctypes.data_as(_dp), len(rows), C.byref(tl),
+                             nx.ctypes.data_as(_dp), ny.ctypes.data_as(_dp), C.byref(n_out)),
+           "pp_plan_frame")
+    n = n_out.value
+    return nx[:n].copy(), ny[:n].copy(), tl.value
+
+
+DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
+
+
+def highway_map():
+    """x, y of the reference's data/highway_map.csv (the only columns the path reads,
+    src/main.cpp:1181-1193), stored as float64 in data/highway_map.npz."""
+    z = np.load(os.path.join(DATA_DIR, "highway_map.npz"))
+    return z["x"].copy(), z["y"].copy()
+
+
+def version() -> str:
+    return lib.pp_version().decode()

@@ -1,0 +1,197 @@
+/*
+ * pp.h — C-ABI of the MI355X batched trajectory-candidate evaluator.
+ *
+ * This header is the drop-in boundary. It replaces the reference's per-frame websocket glue
+ * (Fable3/CarND-Path-Planning-Project, src/main.cpp:1214-1474: the uWS `onMessage` lambda that
+ * parses telemetry, runs the planner and replies with next_x/next_y) by a batch interface:
+ * many scenes in, per-candidate costs + one winning next_x/next_y path per scene out.
+ *
+ *   reference interface                         replaced by
+ *   ------------------------------------------  -----------------------------------------------
+ *   main(): CSV load + Map::Init                pp_map_create / pp_map_destroy
+ *     (src/main.cpp:1160-1193, 89-131)
+ *   onMessage compute body (src/main.cpp:       pp_eval (batched, device-resident SoA buffers)
+ *     1229-1457) for ONE telemetry frame        pp_plan_frame (one frame, host buffers — the
+ *                                                 literal onMessage replacement, C = 1)
+ *   TrajectoryBuilder::build (src/main.cpp:     every candidate (lane, speed) of pp_eval runs this
+ *     565-1049)                                   exact algorithm; see DESIGN.md
+ *
+ * Plain C: no torch or HIP types cross this boundary. Device pointers are `void*`/typed pointers
+ * into HIP device memory (hipMalloc, or torch tensors' data_ptr()). Every entry point returns an
+ * int32 status (PP_OK = 0, negative on error) and never throws.
+ */
+#ifndef PP_H
+#define PP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- fixed sizes ------------------------------------------------------------------------- */
+#define PP_NUM_LANES   3    /* src/main.cpp:22 NUM_LANES                                      */
+#define PP_PREV_KEEP   10   /* src/main.cpp:1258 prev_trajectory_length                       */
+#define PP_MAX_CARS    16   /* sensor_fusion rows per scene (simulator sends 12)              */
+#define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
+#define PP_MAX_POINTS  128  /* horizon N upper bound (reference: 50, src/main.cpp:854,1039)   */
+#define PP_MAX_KNOTS   16   /* spline knots: 9 prev + 1 + 5 control points (src/main.cpp:744) */
+
+/* ---- status codes ------------------------------------------------------------------------ */
+#define PP_OK              0
+#define PP_ERR_ARG        -1   /* null pointer / out-of-range size                              */
+#define PP_ERR_HIP        -2   /* HIP runtime error                                            */
+#define PP_ERR_NOMEM      -3
+#define PP_ERR_NODEVICE   -4
+
+/* ---- per-scene status flags (pp_result.status) -------------------------------------------- */
+#define PP_ST_EGO_UNMATCHED  (1u << 0)  /* src/main.cpp:1302-1307 "can't lane match ego"        */
+#define PP_ST_CAR_UNMATCHED  (1u << 1)  /* src/main.cpp:1336-1340 car erased                    */
+#define PP_ST_FALLBACK       (1u << 2)  /* some candidate used the fallback integrator :848     */
+#define PP_ST_SPLINE_TRUNC   (1u << 3)  /* some candidate truncated non-monotone knots :833     */
+#define PP_ST_NAN            (1u << 4)  /* some candidate produced a NaN cost / bounded walk hit */
+#define PP_ST_COLLISION      (1u << 5)  /* LimitSpeed negative gap :1075-1079                   */
+#define PP_ST_ACC_OVERRIDE   (1u << 6)  /* some candidate hit the accT override :945-971        */
+#define PP_ST_CURV_ADJUST    (1u << 7)  /* some candidate hit the curvature adjust :972-1018    */
+#define PP_ST_TOO_FAR        (1u << 8)  /* "target lane too far" rule fired :1358-1369          */
+#define PP_ST_BRAKE          (1u << 9)  /* a LimitSpeed returned BRAKE :1109                    */
+#define PP_ST_MAXBRAKE       (1u << 10) /* a LimitSpeed returned MAXBRAKE :1101                 */
+#define PP_ST_ADJUST         (1u << 11) /* a LimitSpeed returned ADJUST :1131                   */
+#define PP_ST_KEEP           (1u << 12) /* a LimitSpeed returned KEEP :1146                     */
+#define PP_ST_LANE_CLOSED    (1u << 13) /* some lane was closed by the planner :405-444         */
+#define PP_ST_JUMP_RULE      (1u << 14) /* two-lane jump replaced by adjacent/ego lane :473-479 */
+
+/* ---- cost modes --------------------------------------------------------------------------- */
+/* PP_COST_REFERENCE: the reference's decision (planner lane, max_speed) always wins; the other
+ *   candidates are ranked behind it by the comfort term. winner's next_x/next_y == reference.
+ * PP_COST_COMFORT: pure comfort/lane-score cost, argmin is data dependent. */
+#define PP_COST_REFERENCE 0
+#define PP_COST_COMFORT   1
+
+/* ---- scene batch (SoA; all arrays caller owned, device resident for pp_eval) ------------- */
+/* Index conventions: per-scene scalars [s]; prev points [i * n_scenes + s] (i < PP_PREV_KEEP);
+ * cars [j * n_scenes + s] (j < car_stride). Car ids of one scene must be ascending over j < n_cars
+ * (the reference iterates a std::map<int, Car>, src/main.cpp:1194, 377, 1388). */
+typedef struct pp_scene_batch {
+    int64_t n_scenes;
+    int32_t car_stride;            /* number of car columns (<= PP_MAX_CARS)                  */
+    int32_t _pad;
+    const double*  ego_x;          /* telemetry x, src/main.cpp:1233                           */
+    const double*  ego_y;          /* telemetry y                                              */
+    const double*  ego_yaw_deg;    /* telemetry yaw (degrees)                                  */
+    const double*  ego_speed_mph;  /* telemetry speed (mph), /2.237 at src/main.cpp:1239       */
+    const double*  prev_x;         /* previous_path_x[0..9]                                    */
+    const double*  prev_y;         /* previous_path_y[0..9]                                    */
+    const int32_t* n_prev;         /* previous_path size (>=10 => first 10 used, else none)    */
+    const int32_t* prev_target_lane; /* the cross-frame `target_lane` capture, src/main.cpp:1195 */
+    const int32_t* n_cars;         /* sensor_fusion rows used (<= car_stride)                  */
+    const int32_t* car_id;
+    const double*  car_x;
+    const double*  car_y;
+    const double*  car_vx;
+    const double*  car_vy;
+} pp_scene_batch;
+
+/* ---- parameters ---------------------------------------------------------------------------- */
+typedef struct pp_params {
+    int32_t n_points;      /* horizon N incl. kept previous points (reference 50)            */
+    int32_t n_speeds;      /* speeds per lane: k = 0 is max_speed, k >= 1 uses speed_offsets   */
+    int32_t cost_mode;     /* PP_COST_REFERENCE | PP_COST_COMFORT                             */
+    int32_t emit_paths;    /* 1: write every candidate's path to pp_result.paths              */
+    double  speed_offsets[PP_MAX_SPEEDS]; /* v_k = clamp(ego_speed + speed_offsets[k-1], 0, max_speed) */
+    /* tunables, src/main.cpp:39-49 (defaults = reference values) */
+    double  relaxed_acc;                    /* 5    */
+    double  min_relaxed_acc_while_braking;  /* 4    */
+    double  maximum_acc;                    /* 8    */
+    double  max_speed;                      /* 22.2 */
+    double  car_length;                     /* 4.5  */
+    double  safety_distance;                /* 2    */
+    double  keep_distance;                  /* 10   */
+    double  keep_distance_leeway;           /* 0.5  */
+} pp_params;
+
+/* ---- optional per-scene diagnostics (the planner's intermediate state) --------------------- */
+typedef struct pp_scene_info {
+    double  ego_x, ego_y, ego_speed, ego_acc;      /* after the derivation, src/main.cpp:1261-1320 */
+    double  ego_s, ego_d, ego_vs, ego_vd;
+    double  ref_ratio[PP_NUM_LANES];               /* Map::reference_waypoint_ratio          */
+    double  lane_score[PP_NUM_LANES];              /* LaneChangePlanner scores :450-471       */
+    int32_t ref_wp;                                /* Map::reference_waypoint_id             */
+    int32_t ego_lane;
+    int32_t target_lane;                           /* after planner + too-far rule           */
+    int32_t lane_open_mask;
+    int32_t n_matched_cars;
+    int32_t in_lane_car;                           /* follow car id or -1, :1383-1400         */
+    int32_t _pad[2];
+} pp_scene_info;
+
+/* ---- results (caller owned; device resident for pp_eval) ---------------------------------- */
+/* C = PP_NUM_LANES * n_speeds, candidate c = lane * n_speeds + k.
+ * next_x/next_y: [s * n_points + i]; cost: [s * C + c];
+ * paths (emit_paths): [((s * n_points + i) * C + c) * 2 + {0:x, 1:y}], path_len: [s * C + c]. */
+typedef struct pp_result {
+    int32_t*  winner;
+    int32_t*  n_out;          /* points written to next_x/next_y for the scene (<= n_points)  */
+    double*   next_x;
+    double*   next_y;
+    double*   cost;
+    uint32_t* status;
+    double*   paths;          /* optional (emit_paths)                                          */
+    int32_t*  path_len;       /* optional (emit_paths)                                          */
+    pp_scene_info* info;      /* optional                                                       */
+} pp_result;
+
+/* ---- API ----------------------------------------------------------------------------------- */
+typedef struct pp_map pp_map;
+
+void    pp_params_default(pp_params* p);
+int32_t pp_num_candidates(const pp_params* p);
+
+/* Map::Init (src/main.cpp:89-131) on the host; the lane geometry is uploaded lazily per device. */
+int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out);
+int32_t pp_map_destroy(pp_map* m);
+/* host copy of the derived geometry: per waypoint {ref.x, ref.y, nx, ny, lc0.x, lc0.y, lc1.x,
+ * lc1.y, lc2.x, lc2.y} (10 doubles) — the Map::Init known-answer output. */
+int32_t pp_map_geometry(const pp_map* m, double* out10, int32_t n);
+
+/* Pre-size the per-device workspace (optional; pp_eval grows it on demand, which allocates). */
+int32_t pp_reserve(pp_map* m, int32_t device, int64_t max_scenes);
+
+/* Evaluate a batch. All batch/result pointers are device memory on `device`; `hip_stream` is a
+ * hipStream_t (NULL = default stream). Asynchronous w.r.t. the host. */
+int32_t pp_eval(pp_map* m, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
+                int32_t device, void* hip_stream);
+
+/* One telemetry frame, host memory in/out: the onMessage replacement (C = 1, reference decision).
+ * prev_x/prev_y hold n_prev points (only the first 10 are read when n_prev >= 10); the car arrays
+ * hold n_cars rows in any order (sorted by id internally, as std::map does).
+ * *target_lane is read (cross-frame state) and updated. Writes up to 50 points. */
+int32_t pp_plan_frame(pp_map* m, int32_t device,
+                      double ego_x, double ego_y, double ego_yaw_deg, double ego_speed_mph,
+                      const double* prev_x, const double* prev_y, int32_t n_prev,
+                      const int32_t* car_id, const double* car_x, const double* car_y,
+                      const double* car_vx, const double* car_vy, int32_t n_cars,
+                      int32_t* target_lane, double* next_x, double* next_y, int32_t* n_out);
+
+/* Deterministic synthetic scenes (Philox4x32-10 keyed by seed, counter = global scene index),
+ * generated on `device` into caller-owned device buffers described by `out` (car_stride = 12).
+ * first_scene = global index of out's scene 0 (for multi-GPU shards). */
+int32_t pp_synth_scenes(pp_map* m, uint64_t seed, int64_t first_scene, pp_scene_batch* out,
+                        int32_t device, void* hip_stream);
+/* The same generator on the host (identical bits except ego_yaw_deg, which goes through atan2). */
+int32_t pp_synth_scenes_host(const pp_map* m, uint64_t seed, int64_t first_scene,
+                             pp_scene_batch* out);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
+ * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the
+ * summed milliseconds and launch counts per kernel, and clears the record. */
+int32_t pp_timing_enable(pp_map* m, int32_t device, int32_t enable);
+int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches3);
+
+/* Library version / build info string. */
+const char* pp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PP_H */

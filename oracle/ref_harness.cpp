@@ -1,0 +1,180 @@
+
+// ---- oracle/ref_harness.cpp — TEST INFRASTRUCTURE ONLY -------------------------------------
+// Appended (by oracle/Makefile) after the reference's src/main.cpp:22-1154, so the classes used
+// below are the reference's own. This restates the compute body of the onMessage lambda
+// (src/main.cpp:1233-1448) for one telemetry frame per scene, with a fresh sensor_fusion_cars map
+// per scene, and additionally runs every (lane, speed) candidate through the same classes.
+#include "include/pp.h"
+
+namespace refh {
+
+struct Cand { double sc_target; int lane; };
+
+static void select_follow(std::map<int, Car>& cars, double delta_t0, double ego_s, double ego_d,
+                          double d_target, int& in_id, double& in_s, int& t_id, double& t_s) {
+    // src/main.cpp:1383-1411 (verbatim logic, target lane parameterised)
+    in_id = -1; in_s = 0; t_id = -1; t_s = 0;
+    for (auto& p : cars) {
+        auto& other = p.second;
+        double s0 = other.predicted_s(delta_t0);
+        double d0 = other.predicted_d(delta_t0);
+        if (s0 > ego_s && fabs(d0 - ego_d) < 3) {
+            if (in_id == -1 || in_s > s0) { in_id = other.id; in_s = s0; }
+        }
+        if (s0 >= ego_s - car_length - safety_distance && fabs(d0 - d_target) < 3) {
+            if (t_id == -1 || t_s > s0) { t_id = other.id; t_s = s0; }
+        }
+    }
+    if (t_id == in_id) t_id = -1;
+}
+
+static void apply_limits(std::map<int, Car>& cars, SpeedController& sc, int in_id, double in_s,
+                         int t_id, double t_s, double ego_s, double ego_speed, double ego_acc) {
+    if (in_id != -1) {                                                   // :1425-1431
+        LimitSpeed ls;
+        auto& fc = cars[in_id];
+        ls.calculate(fc, in_s, ego_s, ego_speed, ego_acc, true);
+        sc.add_limit_breakpoint(ls.target_speed, ls.target_time);
+    }
+    if (t_id != -1) {                                                    // :1432-1438
+        LimitSpeed ls;
+        auto& fc = cars[t_id];
+        ls.calculate(fc, t_s, ego_s, ego_speed, ego_acc, false);
+        sc.add_limit_breakpoint(ls.target_speed, ls.target_time);
+    }
+}
+
+}  // namespace refh
+
+// Outputs (all host, caller-allocated):
+//   ref_next [S][50][2], ref_n [S], ref_T [S]          : the reference frame's own trajectory
+//   paths [S][C][50][2] (NaN padded), path_len [S][C]  : every candidate (lane, speed)
+//   info [S][8]: ego_s, ego_d, ego_vs, ego_vd, ego_speed, ego_acc, ego_lane, ref_wp
+extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_scene_batch* in,
+                        int n_speeds, const double* speed_offsets, int with_frame,
+                        double* ref_next, int* ref_n,
+                        int* ref_T, double* paths, int* path_len, double* info) {
+    Map map;
+    vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
+    map.Init(X, Y);
+    const int64_t S = in->n_scenes;
+    const int C = 3 * n_speeds;
+    for (int64_t s = 0; s < S; s++) {
+        double ego_x = in->ego_x[s];
+        double ego_y = in->ego_y[s];
+        double ego_yaw = in->ego_yaw_deg[s];
+        double ego_speed = in->ego_speed_mph[s];
+        ego_speed /= 2.237;
+        double ego_acc = 0;
+        vector<Point> prev_trajectory;
+        double delta_t0 = 0;
+        Point ego_speed_vector;
+        int prev_trajectory_length = 10;
+        if (in->n_prev[s] >= prev_trajectory_length) {                   // :1261-1282
+            for (int i = 0; i < prev_trajectory_length; i++)
+                prev_trajectory.push_back(Point(in->prev_x[i * S + s], in->prev_y[i * S + s]));
+            double v2 = (prev_trajectory[prev_trajectory_length - 2] - prev_trajectory[prev_trajectory_length - 3]).length();
+            ego_speed_vector = prev_trajectory[prev_trajectory_length - 1] - prev_trajectory[prev_trajectory_length - 2];
+            double v3 = ego_speed_vector.length();
+            ego_acc = (v3 - v2) * 50;
+            ego_speed = v3 * 50;
+            ego_speed_vector.x *= 50;
+            ego_speed_vector.y *= 50;
+            ego_x = prev_trajectory[prev_trajectory_length - 1].x;
+            ego_y = prev_trajectory[prev_trajectory_length - 1].y;
+            delta_t0 = prev_trajectory_length / 50.0;
+        } else if (jump_to_waypoint) {
+            Point p = map.get_waypoint(jump_to_waypoint).lane_center[1];
+            ego_x = p.x;
+            ego_y = p.y;
+        }
+        map.init_reference_waypoint(ego_x, ego_y);                       // :1299
+        int ego_lane;
+        double ego_s, ego_d;
+        if (!map.lane_matching(ego_x, ego_y, ego_s, ego_d, ego_lane)) {
+            ego_s = ego_d = 0;
+            ego_lane = 0;
+        }
+        double ego_vs, ego_vd;
+        map.project_speed(ego_speed_vector, map.reference_waypoint_id, &ego_vs, &ego_vd);
+        if (ego_acc > maximum_acc) ego_acc = maximum_acc;
+        if (ego_acc < -maximum_acc) ego_acc = -maximum_acc;
+        std::map<int, Car> sensor_fusion_cars;                           // :1325-1350
+        int ncar = in->n_cars[s] < in->car_stride ? in->n_cars[s] : in->car_stride;
+        for (int j = 0; j < ncar; j++) {
+            int id = in->car_id[j * S + s];
+            auto& car = sensor_fusion_cars[id];
+            car.id = id;
+            car.x = in->car_x[j * S + s];
+            car.y = in->car_y[j * S + s];
+            car.vx = in->car_vx[j * S + s];
+            car.vy = in->car_vy[j * S + s];
+            int next_wp_id = 0;
+            if (!map.lane_matching(car.x, car.y, car.s, car.d, car.lane, &next_wp_id))
+                sensor_fusion_cars.erase(sensor_fusion_cars.find(id));
+            else
+                map.project_speed(Point(car.vx, car.vy), next_wp_id, &car.vs, &car.vd);
+        }
+        int target_lane = in->prev_target_lane[s];
+        LaneChangePlanner lane_change_planner;                           // :1352-1356
+        target_lane = lane_change_planner.calculate_target_lane(sensor_fusion_cars, ego_lane,
+                                                                target_lane, ego_s, ego_vs, delta_t0);
+        if (target_lane != ego_lane) {                                   // :1358-1369
+            double d_of_target_lane = map.get_lane_center_offset(target_lane);
+            double predict_t = 1.0;
+            double lane_d_diff = fabs(ego_vd * predict_t + ego_d - d_of_target_lane);
+            if (lane_d_diff > 6.0) target_lane = ego_lane;
+        }
+        // the reference frame's own trajectory (:1383-1457)
+        if (with_frame) {
+            int in_id, t_id;
+            double in_s, t_s;
+            refh::select_follow(sensor_fusion_cars, delta_t0, ego_s, ego_d,
+                                map.get_lane_center_offset(target_lane), in_id, in_s, t_id, t_s);
+            SpeedController speed_controller(ego_speed);
+            refh::apply_limits(sensor_fusion_cars, speed_controller, in_id, in_s, t_id, t_s, ego_s,
+                               ego_speed, ego_acc);
+            TrajectoryBuilder trajectory;
+            vector<Point> r = trajectory.build(prev_trajectory, ego_x, ego_y, ego_yaw, ego_lane,
+                                               target_lane, ego_d, ego_vd, map, speed_controller);
+            ref_n[s] = (int)r.size();
+            ref_T[s] = target_lane;
+            for (int i = 0; i < 50; i++) {
+                ref_next[(s * 50 + i) * 2 + 0] = i < (int)r.size() ? r[i].x : 0.0;
+                ref_next[(s * 50 + i) * 2 + 1] = i < (int)r.size() ? r[i].y : 0.0;
+            }
+        }
+        // every candidate (lane L, speed k): SpeedController with target v (k = 0: max_speed)
+        for (int c = 0; c < C; c++) {
+            int L = c / n_speeds, k = c % n_speeds;
+            double v = max_speed;
+            if (k > 0) {
+                v = ego_speed + speed_offsets[k - 1];
+                if (v < 0) v = 0;
+                if (v > max_speed) v = max_speed;
+            }
+            int in_id, t_id;
+            double in_s, t_s;
+            refh::select_follow(sensor_fusion_cars, delta_t0, ego_s, ego_d,
+                                map.get_lane_center_offset(L), in_id, in_s, t_id, t_s);
+            SpeedController sc(ego_speed);
+            sc.target_speed = v;
+            sc.target_time = fabs(ego_speed - v) / relaxed_acc;
+            refh::apply_limits(sensor_fusion_cars, sc, in_id, in_s, t_id, t_s, ego_s, ego_speed, ego_acc);
+            TrajectoryBuilder tb;
+            vector<Point> r = tb.build(prev_trajectory, ego_x, ego_y, ego_yaw, ego_lane, L, ego_d,
+                                       ego_vd, map, sc);
+            path_len[s * C + c] = (int)r.size();
+            for (int i = 0; i < 50; i++) {
+                double px = i < (int)r.size() ? r[i].x : NAN;
+                double py = i < (int)r.size() ? r[i].y : NAN;
+                paths[((s * C + c) * 50 + i) * 2 + 0] = px;
+                paths[((s * C + c) * 50 + i) * 2 + 1] = py;
+            }
+        }
+        double* I = info + s * 8;
+        I[0] = ego_s; I[1] = ego_d; I[2] = ego_vs; I[3] = ego_vd; I[4] = ego_speed; I[5] = ego_acc;
+        I[6] = ego_lane; I[7] = map.reference_waypoint_id;
+    }
+    return 0;
+}

@@ -1,0 +1,196 @@
+"""Generate the golden fixtures in tests/golden/ (run in the build container, where
+/root/reference exists). Committed together with its outputs; the GPU box only reads the .npz.
+
+Outputs
+- ../../carnd-path-planning-project_amd/data/highway_map.npz : x, y columns of the reference's data/highway_map.csv (the only map columns
+                      the path reads, src/main.cpp:1181-1193), parsed as the reference parses them.
+- drawlines_lanes.npz: lane0/lane1/lane2 arrays (181 x 2, 4 dp) from the reference's own
+                      DrawLines.ipynb — the Map::Init known-answer fixture.
+- golden_scenes.npz : scenes (SoA inputs) + the outputs of the REFERENCE'S OWN CODE
+                      (oracle/_ref/libppref.so built from /root/reference/src by oracle/Makefile):
+                      the frame's own trajectory, every (lane, speed) candidate path, ego state;
+                      plus the C restatement's costs/winners/status (cost is a build extension
+                      with no reference counterpart). Scenes = random synthetic scenes +
+                      branch-coverage scenes picked greedily from a stress pool by status flag.
+
+Usage: python tests/golden/make_golden.py   (after `make -C oracle`)
+"""
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+import oracle_lib  # noqa: E402
+from oracle_lib import ppamd  # noqa: E402
+
+REF = "/root/reference"
+SPEED_OFFSETS = [-4.0, -2.0, 0.0, 2.0]
+N_SPEEDS = 5
+
+
+def write_map():
+    xs, ys = [], []
+    with open(os.path.join(REF, "data", "highway_map.csv")) as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) < 2:
+                continue
+            xs.append(float(parts[0]))   # iss >> double (exact decimal -> double)
+            ys.append(float(parts[1]))
+    np.savez(os.path.join(os.path.dirname(os.path.dirname(HERE)), "carnd-path-planning-project_amd",
+                          "data", "highway_map.npz"), x=np.array(xs), y=np.array(ys))
+    return np.array(xs), np.array(ys)
+
+
+def write_drawlines():
+    nb = json.load(open(os.path.join(REF, "DrawLines.ipynb")))
+    src = "".join(nb["cells"][1]["source"])
+    out = {}
+    for name in ["lane0", "lane1", "lane2", "wpmap"]:
+        m = re.search(r"^%s=(\[.*?\]\])" % name, src, re.M)
+        out[name] = np.array(json.loads(m.group(1)), np.float64)
+    np.savez(os.path.join(HERE, "drawlines_lanes.npz"), **out)
+    return out
+
+
+def stress_pool(m, wx, wy, S, seed):
+    """Synthetic scenes pushed towards rare branches (numpy edits of synthesized scenes)."""
+    rng = np.random.default_rng(seed)
+    d = ppamd.synth_host(m, S, seed=seed, first=0)
+    p9x, p9y = d["prev_x"][9].copy(), d["prev_y"][9].copy()
+    ux, uy = p9x - d["prev_x"][8], p9y - d["prev_y"][8]
+    nrm = np.hypot(ux, uy)
+    yaw = np.deg2rad(d["ego_yaw_deg"])
+    ux = np.where(nrm > 1e-6, ux / np.maximum(nrm, 1e-12), np.cos(yaw))
+    uy = np.where(nrm > 1e-6, uy / np.maximum(nrm, 1e-12), np.sin(yaw))
+    nx, ny = uy, -ux                                     # +d direction
+    kind = rng.integers(0, 9, S)
+    for s in range(S):
+        k = kind[s]
+        if k == 0:      # frame 0 (telemetry pose only), any speed incl. 0
+            d["n_prev"][s] = 0
+            if rng.random() < 0.3:
+                d["ego_speed_mph"][s] = 0.0
+        elif k == 1:    # off-road: shift the whole ego state by 18..30 m sideways
+            off = rng.uniform(18, 30) * rng.choice([-1, 1])
+            d["prev_x"][:, s] += nx[s] * off
+            d["prev_y"][:, s] += ny[s] * off
+            d["ego_x"][s] += nx[s] * off
+            d["ego_y"][s] += ny[s] * off
+        elif k == 2:    # heading mismatch: rotate the previous path about p9
+            th = np.deg2rad(rng.uniform(20, 160) * rng.choice([-1, 1]))
+            c, sn = np.cos(th), np.sin(th)
+            dx, dy = d["prev_x"][:, s] - p9x[s], d["prev_y"][:, s] - p9y[s]
+            d["prev_x"][:, s] = p9x[s] + c * dx - sn * dy
+            d["prev_y"][:, s] = p9y[s] + sn * dx + c * dy
+        elif k == 3:    # lateral drift: small rotation => ego_vd
+            th = np.deg2rad(rng.uniform(-12, 12))
+            c, sn = np.cos(th), np.sin(th)
+            dx, dy = d["prev_x"][:, s] - p9x[s], d["prev_y"][:, s] - p9y[s]
+            d["prev_x"][:, s] = p9x[s] + c * dx - sn * dy
+            d["prev_y"][:, s] = p9y[s] + sn * dx + c * dy
+        elif k == 4:    # dense traffic: cars placed around the ego along its heading
+            lane_e = rng.integers(0, 3)
+            for j in range(12):
+                ds = rng.uniform(-25, 35)
+                cl = rng.integers(0, 3)
+                lat = 4.0 * (cl - lane_e) + rng.uniform(-0.4, 0.4)
+                sp = rng.uniform(0, 25)
+                d["car_x"][j, s] = p9x[s] + ux[s] * ds + nx[s] * lat
+                d["car_y"][j, s] = p9y[s] + uy[s] * ds + ny[s] * lat
+                d["car_vx"][j, s] = ux[s] * sp
+                d["car_vy"][j, s] = uy[s] * sp
+        elif k == 5:    # standing still: all previous points equal
+            d["prev_x"][:, s] = p9x[s]
+            d["prev_y"][:, s] = p9y[s]
+        elif k == 6:    # ego far from the map -> unmatched
+            off = rng.uniform(1500, 4000)
+            d["prev_x"][:, s] += off
+            d["ego_x"][s] += off
+        elif k == 7:    # sparse / reordered sensor fusion: fewer cars, gappy ascending ids
+            nc = int(rng.integers(0, 12))
+            ids = np.sort(rng.choice(100, 12, replace=False)).astype(np.int32)
+            d["car_id"][:, s] = ids
+            d["n_cars"][s] = nc
+        else:           # fast cars close behind + slow car just ahead in every lane
+            for j in range(6):
+                ds = rng.uniform(-30, -3) if j % 2 == 0 else rng.uniform(3, 18)
+                lat = 4.0 * (j % 3 - 1) + rng.uniform(-0.3, 0.3)
+                sp = rng.uniform(20, 30) if j % 2 == 0 else rng.uniform(0, 8)
+                d["car_x"][j, s] = p9x[s] + ux[s] * ds + nx[s] * lat
+                d["car_y"][j, s] = p9y[s] + uy[s] * ds + ny[s] * lat
+                d["car_vx"][j, s] = ux[s] * sp
+                d["car_vy"][j, s] = uy[s] * sp
+    return d, kind
+
+
+def take(d, idx):
+    out = {}
+    for k, v in d.items():
+        out[k] = np.ascontiguousarray(v[..., idx]) if v.ndim == 2 else np.ascontiguousarray(v[idx])
+    return out
+
+
+def main():
+    wx, wy = write_map()
+    write_drawlines()
+    m = ppamd.Map(wx, wy)
+    olib = oracle_lib.load_oracle()
+    rlib = oracle_lib.load_ref()
+    assert rlib is not None, "build oracle/_ref first: make -C oracle"
+    prm = ppamd.default_params(n_speeds=N_SPEEDS, speed_offsets=SPEED_OFFSETS, emit_paths=True)
+
+    # random synthetic scenes (the bench distribution, seed 7)
+    rand = ppamd.synth_host(m, 160, seed=7, first=0)
+    # coverage: greedy pick by status flag from a stress pool
+    pool, kind = stress_pool(m, wx, wy, 6000, seed=11)
+    pres = oracle_lib.oracle_eval(olib, wx, wy, pool, prm)
+    st = pres["status"].view(np.uint32)
+    picked = []
+    for name, bit in ppamd.STATUS_BITS.items():
+        hits = np.nonzero(st & bit)[0]
+        for i in hits[:6]:
+            if i not in picked:
+                picked.append(int(i))
+        print(f"coverage {name:14s}: {len(hits):5d} pool hits")
+    for kk in range(9):                       # a few of every stress kind
+        for i in np.nonzero(kind == kk)[0][:4]:
+            if int(i) not in picked:
+                picked.append(int(i))
+    cov = take(pool, np.array(picked))
+    scenes = {k: np.concatenate([rand[k], cov[k]], axis=-1) for k in rand}
+    S = scenes["ego_x"].shape[0]
+    print("golden scenes:", S, "(random 160 + coverage", len(picked), ")")
+
+    ref = oracle_lib.ref_eval(rlib, wx, wy, scenes, N_SPEEDS, SPEED_OFFSETS)
+    ores = oracle_lib.oracle_eval(olib, wx, wy, scenes, prm)
+    # the restatement must equal the reference bit for bit on every candidate path
+    op = np.transpose(ores["paths"], (0, 2, 1, 3))   # [S][C][N][2]
+    same = (op == ref["paths"]) | (np.isnan(op) & np.isnan(ref["paths"]))
+    assert same.all(), f"oracle != reference on {np.count_nonzero(~same)} values"
+    assert (ores["path_len"] == ref["path_len"]).all()
+    # the reference frame's own trajectory == candidate (T, max_speed)
+    T = ref["ref_T"]
+    assert (ores["info"]["target_lane"] == T).all()
+    assert (ores["winner"] == T * N_SPEEDS).all()
+    wn = np.stack([ores["next_x"], ores["next_y"]], -1)
+    assert (wn == ref["ref_next"]).all() and (ores["n_out"] == ref["ref_n"]).all()
+    np.savez_compressed(
+        os.path.join(HERE, "golden_scenes.npz"),
+        **{"scene_" + k: v for k, v in scenes.items()},
+        ref_next=ref["ref_next"], ref_n=ref["ref_n"], ref_T=ref["ref_T"], ref_paths=ref["paths"],
+        ref_path_len=ref["path_len"], ref_info=ref["info"], oracle_cost=ores["cost"],
+        oracle_winner=ores["winner"], oracle_status=ores["status"].view(np.uint32),
+        speed_offsets=np.array(SPEED_OFFSETS), n_speeds=np.array(N_SPEEDS))
+    flags = ores["status"].view(np.uint32)
+    for name, bit in ppamd.STATUS_BITS.items():
+        print(f"golden {name:14s}: {np.count_nonzero(flags & bit)}")
+    print("oracle == reference (bit-exact) on", S, "scenes x", 3 * N_SPEEDS, "candidates")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+"""ctypes loaders for the parity checkers under oracle/ (TEST INFRASTRUCTURE ONLY).
+
+- ``oracle/liboracle.so``: C restatement of the reference loop (oracle/pp_oracle.c); travels to
+  the GPU box.
+- ``oracle/_ref/libppref.so``: the reference's own planning classes (src/main.cpp:22-1154,
+  helpers.h, spline.h) compiled from /root/reference by oracle/Makefile; used to generate and
+  re-check the golden fixtures where the reference exists.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "carnd-path-planning-project_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+import ppamd  # noqa: E402  (structures shared with the C-ABI)
+
+ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
+REF_SO = os.path.join(REPO, "oracle", "_ref", "libppref.so")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+_dp = C.POINTER(C.c_double)
+
+
+def load_oracle():
+    lib = C.CDLL(ORACLE_SO)
+    lib.ppo_eval_range.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch),
+                                   C.POINTER(ppamd.Params), C.POINTER(ppamd.Result), C.c_int64,
+                                   C.c_int64]
+    lib.ppo_eval_range.restype = C.c_int
+    lib.ppo_map_geometry.argtypes = [_dp, _dp, C.c_int, _dp]
+    lib.ppo_map_geometry.restype = C.c_int
+    lib.ppo_struct_sizes.argtypes = [C.POINTER(C.c_int64)]
+    return lib
+
+
+def load_ref():
+    if not os.path.exists(REF_SO):
+        return None
+    lib = C.CDLL(REF_SO)
+    lib.ref_eval.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.c_int, _dp, C.c_int, _dp,
+                             C.POINTER(C.c_int), C.POINTER(C.c_int), _dp, C.POINTER(C.c_int), _dp]
+    lib.ref_eval.restype = C.c_int
+    return lib
+
+
+def highway_map():
+    return ppamd.highway_map()
+
+
+def oracle_eval(lib, wx, wy, scenes, prm, begin=0, end=None, info=True):
+    """Run the C restatement on host SoA scenes; returns a numpy result dict."""
+    S = int(scenes["ego_x"].shape[0])
+    end = S if end is None else end
+    r = ppamd.alloc_result(S, prm, info=info)
+    if prm.emit_paths:
+        r["paths"][:] = np.nan
+    b = ppamd.scene_struct(scenes)
+    R = ppamd.result_struct(r)
+    wx = np.ascontiguousarray(wx, np.float64)
+    wy = np.ascontiguousarray(wy, np.float64)
+    rc = lib.ppo_eval_range(wx.ctypes.data_as(_dp), wy.ctypes.data_as(_dp), len(wx), C.byref(b),
+                            C.byref(prm), C.byref(R), begin, end)
+    assert rc == 0, rc
+    return r
+
+
+def ref_eval(lib, wx, wy, scenes, n_speeds, speed_offsets, with_frame=True):
+    """Run the reference-compiled checker (N = 50 only: the reference hard-codes it)."""
+    S = int(scenes["ego_x"].shape[0])
+    Cn = 3 * n_speeds
+    out = {"ref_next": np.zeros((S, 50, 2)), "ref_n": np.zeros(S, np.int32),
+           "ref_T": np.zeros(S, np.int32), "paths": np.full((S, Cn, 50, 2), np.nan),
+           "path_len": np.zeros((S, Cn), np.int32), "info": np.zeros((S, 8))}
+    offs = np.zeros(ppamd.MAX_SPEEDS)
+    offs[: len(speed_offsets)] = speed_offsets
+    b = ppamd.scene_struct(scenes)
+    wx = np.ascontiguousarray(wx, np.float64)
+    wy = np.ascontiguousarray(wy, np.float64)
+    ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
+    dp = lambda a: a.ctypes.data_as(_dp)
+    # the reference prints warnings to stdout ("spline input error" ...): silence fd 1
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
+    try:
+        rc = lib.ref_eval(dp(wx), dp(wy), len(wx), C.byref(b), n_speeds, dp(offs), int(with_frame),
+                          dp(out["ref_next"]), ip(out["ref_n"]), ip(out["ref_T"]),
+                          dp(out["paths"]), ip(out["path_len"]), dp(out["info"]))
+    finally:
+        C.CDLL(None).fflush(None)      # drain the reference's printf buffer into /dev/null
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+    assert rc == 0
+    return out
