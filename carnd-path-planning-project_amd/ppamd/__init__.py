@@ -89,6 +89,13 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"ppamd: HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+    # torch (ROCm) bundles its own libamdhip64 (soname libamdhip64.so.7, loaded by path). Load it
+    # first so that our DT_NEEDED libamdhip64.so.7 resolves to that same runtime: two HIP runtimes
+    # in one process do not share device allocations.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     lib.pp_params_default.argtypes = [C.POINTER(Params)]
     lib.pp_params_default.restype = None
