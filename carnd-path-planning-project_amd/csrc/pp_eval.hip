@@ -24,6 +24,7 @@
 
 #include "../../include/pp.h"
 #include "pp_device.h"
+#include "pp_math.h"
 #include "pp_synth.h"
 
 using namespace ppd;
@@ -31,7 +32,13 @@ using namespace ppd;
 // ------------------------------------------------------------------------------------------------
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
-struct MapG { const double* buf; int n; };   // 13 arrays of n: ref_x ref_y nx ny lc_x[3] lc_y[3] llen[3]
+// 13 arrays of n: ref_x ref_y nx ny lc_x[3] lc_y[3] llen[3]
+struct MapG { const double* buf; int n; };
+
+// |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
+// <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
+constexpr double kSlowAngle = 1.0e5;
+constexpr int kLimSlow = 1 << 7;   // internal bit in PrepV.lim_mask
 
 __device__ __forceinline__ MapV map_view(const double* b, int n) {
     MapV m;
@@ -222,11 +229,17 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
         pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
         const double vx = pos_x - p8x, vy = pos_y - p8y;
         if (vx * vx + vy * vy < kEps) angle = yaw * kPi / 180;
-        else angle = atan2(pos_y - p8y, pos_x - p8x);
+        else angle = ppm::atan2_pp(pos_y - p8y, pos_x - p8x);
     }
+    // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
+    // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
+    if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
     pv.pos_x[s] = pos_x; pv.pos_y[s] = pos_y; pv.angle[s] = angle;
-    pv.ca_m[s] = cos(-angle); pv.sa_m[s] = sin(-angle);
-    pv.ca_p[s] = cos(angle);  pv.sa_p[s] = sin(angle);
+    double cm, sm, cp, sp_;
+    ppm::sincos_pp<true>(-angle, sm, cm);
+    ppm::sincos_pp<true>(angle, sp_, cp);
+    pv.ca_m[s] = cm; pv.sa_m[s] = sm;
+    pv.ca_p[s] = cp; pv.sa_p[s] = sp_;
     pv.ego_speed[s] = ego_speed; pv.ego_d[s] = ego_d; pv.ego_vd[s] = ego_vd;
 #pragma unroll
     for (int l = 0; l < 3; l++) { pv.ratio[l * S + s] = ratio[l]; pv.score[l * S + s] = score[l]; }
@@ -377,6 +390,7 @@ struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; };
 
 // Output targets: point g (0-based among generated) goes to wx[g*ws], wy[g*ws] (if wx) and
 // px[g*ps], px[g*ps+1] (if px).
+template <bool kLarge>
 __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double cy, double angle,
                                  double ca0, double sa0, SC sc, int room, double* wx, double* wy,
                                  int64_t ws, double* px, int64_t ps) {
@@ -400,8 +414,8 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
             const double cpd = sqrt(ndx * ndx + ndy * ndy);
             if (cpd < 5) { nc++; continue; }
             cur_t += 0.02;
-            const double nca = atan2(ndy, ndx);
-            const double adiff = fmod(nca - cang + 3 * kPi, 2 * kPi) - kPi;
+            const double nca = ppm::atan2_pp(ndy, ndx);
+            const double adiff = ppm::fmod_2pi(nca - cang + 3 * kPi) - kPi;
             const double min_radius = s_max(10.0, speed * speed / 4);
             const double rps = speed / min_radius;
             const double mas = rps / 50;
@@ -410,8 +424,10 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
             } else {
                 cang += adiff;
             }
-            pos_x += cos(cang) * dstep;
-            pos_y += sin(cang) * dstep;
+            double sc_, cc_;
+            ppm::sincos_pp<kLarge>(cang, sc_, cc_);
+            pos_x += cc_ * dstep;
+            pos_y += sc_ * dstep;
             const double tx = pos_x * ca - pos_y * sa;
             const double ty = pos_x * sa + pos_y * ca;
             if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
@@ -422,9 +438,6 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
         R.ng = ng;
         return R;
     }
-    const double x_first = sl.X[0], x_last = sl.X[nk - 1];
-    const double b0 = sl.B[0], c0 = sl.C[0], y0 = sl.Y[0];
-    const double bl = sl.B[nk - 1], cl = sl.C[nk - 1], yl = sl.Y[nk - 1];
     int cnt = 0;                     // #knots with X < x (std::lower_bound position)
     double arg = 0, prev_speed = sc.start, prev_angle = 0;
     while (arg < 50 && ng < room) {
@@ -437,13 +450,13 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
         const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
         const double h = x - sl.X[idx];
         double y;
-        if (x < x_first) y = (b0 * h + c0) * h + y0;
-        else if (x > x_last) y = (bl * h + cl) * h + yl;
+        if (cnt == 0 && x < sl.X[0]) y = (sl.B[0] * h + sl.C[0]) * h + sl.Y[0];          // left
+        else if (cnt == nk && x > sl.X[nk - 1]) y = (sl.B[idx] * h + sl.C[idx]) * h + sl.Y[idx];  // right
         else y = ((sl.A[idx] * h + sl.B[idx]) * h + sl.C[idx]) * h + sl.Y[idx];
         const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
         double acc = fabs(speed - prev_speed) * 50;
-        const double astep = atan2(y - pos_y, x - pos_x);
-        const double adiff = fmod(astep - prev_angle + 3 * kPi, 2 * kPi) - kPi;
+        const double astep = ppm::atan2_pp(y - pos_y, x - pos_x);
+        const double adiff = ppm::fmod_2pi(astep - prev_angle + 3 * kPi) - kPi;
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
         if (acc + cacc > P.maximum_acc) {
@@ -469,14 +482,14 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
                 tpx = tpx + cx;
                 tpy = tpy + cy;
                 const double vx = cx - tpx, vy = cy - tpy;
-                const double cr = cos(rot), sr = sin(rot);
+                double cr, sr;
+                ppm::sincos_pp<kLarge>(rot, sr, cr);
                 const double rvx = vx * cr - vy * sr;
                 const double rvy = vx * sr + vy * cr;
                 cx = tpx + rvx;
                 cy = tpy + rvy;
                 tangle += rot;
-                ca = cos(tangle);
-                sa = sin(tangle);
+                ppm::sincos_pp<kLarge>(tangle, sa, ca);
                 eff_c = nc;
                 R.flags |= PP_ST_CURV_ADJUST;
             }
@@ -536,6 +549,9 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 // ------------------------------------------------------------------------------------------------
 // K2: candidates
 // ------------------------------------------------------------------------------------------------
+// kSlow = false: every scene except those flagged kLimSlow by k_prep (no library call in the
+// loop, so the register peak stays at the loop's own state); kSlow = true: only flagged scenes.
+template <bool kSlow>
 __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -553,15 +569,19 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
     const int64_t s0 = (int64_t)blockIdx.x * SPB;
     const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
     const int tid = threadIdx.x;
+    if (kSlow) {   // whole block leaves unless one of its scenes is flagged
+        const bool mine = tid < nsc && (pv.lim_mask[s0 + tid] & kLimSlow);
+        if (!__syncthreads_or(mine)) return;
+    }
     if (tid < SPB) sFlags[tid] = 0;
-    if (tid < 3 * nsc) {                                               // phase A
+    if (tid < 3 * nsc && (((pv.lim_mask[s0 + tid / 3] & kLimSlow) != 0) == kSlow)) {   // phase A
         const int j = tid;
         Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j};
         setup_lane(m, P, in, pv, s0 + j / 3, j % 3, sl);
     }
     __syncthreads();
     const int sc_l = tid / C, c = tid - sc_l * C;
-    if (sc_l < nsc) {                                                  // phase B
+    if (sc_l < nsc && (((pv.lim_mask[s0 + sc_l] & kLimSlow) != 0) == kSlow)) {   // phase B
         const int64_t s = s0 + sc_l;
         const int L = c / NS, k = c - L * NS;
         const int j = sc_l * 3 + L;
@@ -588,8 +608,8 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
                 p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
             }
         }
-        const CandRes R = run_candidate(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
-                                        pv.sa_p[s], sc, N - K, wx, wy, 1, px, ps);
+        const CandRes R = run_candidate<kSlow>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
+                                               pv.sa_p[s], sc, N - K, wx, wy, 1, px, ps);
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
                                       pv.ego_lane[s], flags);
@@ -606,7 +626,8 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
-    if (tid < nsc) out.status[s0 + tid] = (uint32_t)pv.status[s0 + tid] | sFlags[tid];
+    if (tid < nsc && (((pv.lim_mask[s0 + tid] & kLimSlow) != 0) == kSlow))
+        out.status[s0 + tid] = (uint32_t)pv.status[s0 + tid] | sFlags[tid];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -641,7 +662,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
         out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
     }
-    const CandRes R = run_candidate(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
+    const CandRes R = run_candidate<true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
                                     pv.sa_p[s], sc, N - K, out.next_x + s * N + K,
                                     out.next_y + s * N + K, 1, nullptr, 0);
     for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
@@ -957,7 +978,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
         const int64_t blocks = (S + spb - 1) / spb;
         if (timing) (void)hipEventRecord(ev[1], st);
-        hipLaunchKernelGGL(k_cand, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        hipLaunchKernelGGL(k_cand<false>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        hipLaunchKernelGGL(k_cand<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K3 (comfort mode)

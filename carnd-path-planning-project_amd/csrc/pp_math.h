@@ -1,0 +1,217 @@
+// pp_math.h — register-light FP64 transcendentals for the candidate loop (gfx950).
+//
+// The ROCm device library's f64 sin/cos carry the large-argument (Payne-Hanek) reduction inline and
+// atan2 a wide argument-reduction tree: together ~80 VGPRs of the loop's register peak (measured
+// with -Rpass-analysis=kernel-resource-usage), which halves occupancy. The planner only feeds them
+// small arguments (headings and turn angles), so these are the classic fdlibm-style algorithms
+// (Cody-Waite reduction by pi/2, minimax kernels, atan with 4-interval reduction), < 1 ulp like
+// glibc's, with the rare large-argument case handed to the device library in a non-inlined call.
+// All arithmetic is plain IEEE double (the library is built with -ffp-contract=off).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ppm {
+
+__device__ __forceinline__ int hiword(double x) { return (int)(__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ unsigned loword(double x) { return (unsigned)__double_as_longlong(x); }
+__device__ __forceinline__ double from_words(int hi, unsigned lo) {
+    return __longlong_as_double(((long long)hi << 32) | (long long)lo);
+}
+
+// ---- sin / cos kernels on [-pi/4, pi/4] with tail y (x + y = reduced argument) -------------
+__device__ __forceinline__ double ksin(double x, double y, bool has_tail) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    const int ix = hiword(x) & 0x7fffffff;
+    if (ix < 0x3e400000) return x;                 // |x| < 2^-27
+    const double z = x * x;
+    const double v = z * x;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    if (!has_tail) return x + v * (S1 + z * r);
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+
+__device__ __forceinline__ double kcos(double x, double y) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const int ix = hiword(x) & 0x7fffffff;
+    if (ix < 0x3e400000) return 1.0;               // |x| < 2^-27
+    const double z = x * x;
+    const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    if (ix < 0x3FD33333) return 1.0 - (0.5 * z - (z * r - x * y));   // |x| < 0.3
+    const double qx = (ix > 0x3fe90000) ? 0.28125 : from_words(ix - 0x00200000, 0u);
+    const double hz = 0.5 * z - qx;
+    const double a = 1.0 - qx;
+    return a - (hz - (z * r - x * y));
+}
+
+__device__ __attribute__((noinline)) void sincos_large(double x, double* s, double* c) {
+    *s = sin(x);
+    *c = cos(x);
+}
+
+// sin and cos of x. Medium-size Cody-Waite reduction (3-part pi/2) for |x| <= 2^19 * pi/2;
+// beyond that the device library's reduction — compiled in only when kLarge (the hot loop is
+// instantiated without it: its arguments are bounded, see kSlowAngle in pp_eval.hip).
+constexpr double kMediumMax = 823549.6;   // < 2^19 * pi/2 (high word 0x413921fb)
+template <bool kLarge = true>
+__device__ __forceinline__ void sincos_pp(double x, double& s, double& c) {
+    const int hx = hiword(x);
+    const int ix = hx & 0x7fffffff;
+    if (ix <= 0x3fe921fb) {                         // |x| <= pi/4
+        s = ksin(x, 0.0, false);
+        c = kcos(x, 0.0);
+        return;
+    }
+    if (ix > 0x413921fb) {                          // huge, inf or NaN
+        if (kLarge) {
+            sincos_large(x, &s, &c);
+        } else {
+            s = c = __builtin_nan("");                 // unreachable by construction
+        }
+        return;
+    }
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+                 pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+                 pio2_3t = 8.47842766036889956997e-32;
+    double t = fabs(x);
+    const int n = (int)(t * invpio2 + 0.5);
+    const double fn = (double)n;
+    double r = t - fn * pio2_1;
+    double w = fn * pio2_1t;                        // first round good to 85 bits
+    const int j = ix >> 20;
+    double y0 = r - w;
+    int i = j - ((hiword(y0) >> 20) & 0x7ff);
+    if (i > 16) {                                   // cancellation: second round, 118 bits
+        t = r;
+        w = fn * pio2_2;
+        r = t - w;
+        w = fn * pio2_2t - ((t - r) - w);
+        y0 = r - w;
+        i = j - ((hiword(y0) >> 20) & 0x7ff);
+        if (i > 49) {                               // third round, 151 bits
+            t = r;
+            w = fn * pio2_3;
+            r = t - w;
+            w = fn * pio2_3t - ((t - r) - w);
+            y0 = r - w;
+        }
+    }
+    double y1 = (r - y0) - w;
+    int q = n;
+    if (hx < 0) { y0 = -y0; y1 = -y1; q = -n; }
+    const double ks = ksin(y0, y1, true);
+    const double kc = kcos(y0, y1);
+    switch (q & 3) {
+        case 0: s = ks; c = kc; break;
+        case 1: s = kc; c = -ks; break;
+        case 2: s = -ks; c = -kc; break;
+        default: s = -kc; c = ks; break;
+    }
+}
+
+// ---- atan / atan2 --------------------------------------------------------------------------
+__device__ __forceinline__ double atan_pos(double x, int ix) {
+    // x >= 0, ix = high word of x; |x| < 2^66
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    int id;
+    double hi = 0, lo = 0;
+    if (ix < 0x3fdc0000) {                          // |x| < 0.4375
+        if (ix < 0x3e400000) return x;              // |x| < 2^-27
+        id = -1;
+    } else if (ix < 0x3ff30000) {                   // |x| < 1.1875
+        if (ix < 0x3fe60000) {                      // 7/16 <= |x| < 11/16
+            id = 0; hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17;
+            x = (2.0 * x - 1.0) / (2.0 + x);
+        } else {                                    // 11/16 <= |x| < 19/16
+            id = 1; hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17;
+            x = (x - 1.0) / (x + 1.0);
+        }
+    } else if (ix < 0x40038000) {                   // |x| < 2.4375
+        id = 2; hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17;
+        x = (x - 1.5) / (1.0 + 1.5 * x);
+    } else {                                        // 2.4375 <= |x| < 2^66
+        id = 3; hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17;
+        x = -1.0 / x;
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    return hi - ((x * (s1 + s2) - lo) - x);
+}
+
+// atan2 for zero / infinite / NaN arguments (C standard Annex F values)
+__device__ __forceinline__ double atan2_special(double y, double x) {
+    const double pi = 3.1415926535897931160E+00, pi_o_2 = 1.5707963267948965580E+00,
+                 pi_o_4 = 7.8539816339744827900E-01;
+    if (x != x || y != y) return x + y;
+    const bool xneg = hiword(x) < 0;
+    const double sy = hiword(y) < 0 ? -1.0 : 1.0;
+    if (y == 0.0) return xneg ? sy * pi : y;                    // atan2(+-0, x)
+    const bool xinf = fabs(x) == __builtin_inf(), yinf = fabs(y) == __builtin_inf();
+    if (yinf && xinf) return xneg ? sy * 3.0 * pi_o_4 : sy * pi_o_4;
+    if (yinf || x == 0.0) return sy * pi_o_2;
+    return xneg ? sy * pi : sy * 0.0;                            // x = +-inf, y finite
+}
+
+// atan2(y, x): quadrant logic of the C standard; finite nonzero arguments take the fast path.
+__device__ __forceinline__ double atan2_pp(double y, double x) {
+    const double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16,
+                 pi_o_2 = 1.5707963267948965580E+00;
+    const int hx = hiword(x), hy = hiword(y);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const bool x_special = (ix | loword(x)) == 0 || ix >= 0x7ff00000;
+    const bool y_special = (iy | loword(y)) == 0 || iy >= 0x7ff00000;
+    if (x_special || y_special) return atan2_special(y, x);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);  // 2*sign(x) + sign(y)
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) {
+        z = pi_o_2 + 0.5 * pi_lo;                    // |y/x| > 2^60
+    } else if (hx < 0 && k < -60) {
+        z = 0.0;                                     // |y|/x < -2^60
+    } else {
+        const double q = fabs(y / x);
+        z = atan_pos(q, hiword(q));
+    }
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// fmod(a, 2*pi) for the reference's angle wrap fmod(d + 3*pi, 2*pi) - pi
+// (src/main.cpp:870, 934). fmod is exact, so any exact evaluation is bit-identical: for
+// 0 <= a < 3*(2*pi) the remainder a - k*(2*pi), k in {0, 1, 2}, is computed exactly
+// (Sterbenz: y <= a < 4y for the k = 2 case, with 2y and 3y exact doubles). Other finite inputs
+// are reduced by exact subtractions of y * 2^j (each r - y*2^j with y*2^j <= r < y*2^(j+1) is
+// exact by Sterbenz), the textbook long division fmod performs.
+__device__ __forceinline__ double fmod_2pi(double a) {
+    const double y = 2 * 3.14159265358979323846;
+    if (a >= 0.0 && a < y) return a;
+    if (a >= y && a < 2.0 * y) return a - y;
+    if (a >= 2.0 * y && a < 3.0 * y) return a - 2.0 * y;
+    if (!(fabs(a) < __builtin_inf())) return a - a;   // inf, NaN -> NaN
+    double r = fabs(a);
+    while (r >= y) {
+        double t = y;
+        while (t * 2.0 <= r) t *= 2.0;
+        r -= t;
+    }
+    return a < 0 ? -r : r;
+}
+
+}  // namespace ppm

@@ -1,0 +1,40 @@
+"""Summarise rocprofv3 --pmc CSVs (tools/pmc.sh) into per-kernel per-launch averages and write
+profiles/pmc_summary.json (read by bench.py for roofline.traffic).
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the bytes of wide
+coalesced streaming reads (x2 applied); WRITE_SIZE is exact for 16-B/lane streaming stores.
+Both counters are in KiB."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+tag = sys.argv[2] if len(sys.argv) > 2 else None
+vals = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
+    for row in csv.DictReader(open(f)):
+        k = row.get("Kernel_Name", "").split("(")[0]
+        vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+summary = {}
+for k, d in vals.items():
+    # rocprofv3 reports one row per dispatch per counter (already summed over XCDs/SEs)
+    summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
+print(json.dumps(summary, indent=1))
+if tag:
+    kc = summary.get("k_cand", {})
+    out = {}
+    p = "profiles/pmc_summary.json"
+    if os.path.exists(p):
+        out = json.load(open(p))
+    fetch = kc.get("FETCH_SIZE")
+    write = kc.get("WRITE_SIZE")
+    if fetch is not None and write is not None:
+        out[tag] = {"hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
+                    "fetch_kib_raw": fetch, "write_kib": write,
+                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({src}); FETCH_SIZE x2 (gfx950)",
+                    "counters": kc}
+        json.dump(out, open(p, "w"), indent=1)
+        print("wrote", p, tag)
