@@ -8,10 +8,9 @@
 //                builds the control points + tk::spline coefficients into LDS
 //                (TrajectoryBuilder::build setup, src/main.cpp:575-904, spline.h:284-373).
 //                Phase B: one lane per candidate runs the 0.02 s resampling loop with the
-//                accel/curvature limiter (src/main.cpp:905-1041) reading its spline from LDS,
-//                computes the candidate cost, and (reference mode) the winning lane writes
-//                next_x/next_y directly.
-//   K3 k_winner  comfort mode only: per-scene argmin + re-run of the winning candidate.
+//                accel/curvature limiter (src/main.cpp:905-1041) reading its spline from LDS
+//                and computes the candidate cost (cost-only loop unless every path is emitted).
+//   K3 k_winner  per-scene argmin + re-run of the winning candidate with outputs (next_x/next_y).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -257,16 +256,26 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
 }
 
 // ------------------------------------------------------------------------------------------------
-// Phase A: control points + spline for one (scene, lane) into an LDS slot
+// Phase A: control points + spline for one (scene, lane) into a slot
 // ------------------------------------------------------------------------------------------------
-struct Slot {          // pointers into LDS, stride kKP per slot
+// A slot holds one spline: knots X/Y and coefficients A/B/C (<= PP_MAX_KNOTS each) + 4 ints.
+// k_cand keeps slots in LDS (stride 1); k_winner in a global scratch laid out [field][knot][S]
+// (stride S: lanes of a wave touch consecutive addresses).
+struct Slot {
     double *X, *Y, *A, *B, *C;
     int* meta;          // [0] n knots, [1] n control points, [2] first control-point knot, [3] flags
+    int64_t st;         // element stride
+    __device__ __forceinline__ double& x(int i) const { return X[i * st]; }
+    __device__ __forceinline__ double& y(int i) const { return Y[i * st]; }
+    __device__ __forceinline__ double& a(int i) const { return A[i * st]; }
+    __device__ __forceinline__ double& b(int i) const { return B[i * st]; }
+    __device__ __forceinline__ double& c(int i) const { return C[i * st]; }
+    __device__ __forceinline__ int& m(int k) const { return meta[k * st]; }
 };
 constexpr int kMetaFallback = 1, kMetaTrunc = 2, kMetaWalkFail = 4;
 
 __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_batch& in,
-                           const PrepV& pv, int64_t s, int L, Slot sl) {
+                           const PrepV& pv, int64_t s, int L, const Slot& sl) {
     const int64_t S = in.n_scenes;
     const int K = pv.K[s];
     const double pos_x = pv.pos_x[s], pos_y = pv.pos_y[s];
@@ -301,13 +310,13 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
     for (int i = 0; i < npk; i++) {
         const double tx0 = in.prev_x[(int64_t)i * S + s] - pos_x;
         const double ty0 = in.prev_y[(int64_t)i * S + s] - pos_y;
-        sl.X[i] = tx0 * ca - ty0 * sa;
-        sl.Y[i] = tx0 * sa + ty0 * ca;
+        sl.x(i) = tx0 * ca - ty0 * sa;
+        sl.y(i) = tx0 * sa + ty0 * ca;
     }
     // control points (:638, 744-768): first = start pose, then get_lane_pos steps
     double lx = pos_x, ly = pos_y, total = 0;
-    sl.X[npk] = (pos_x - pos_x) * ca - (pos_y - pos_y) * sa;
-    sl.Y[npk] = (pos_x - pos_x) * sa + (pos_y - pos_y) * ca;
+    sl.x(npk) = (pos_x - pos_x) * ca - (pos_y - pos_y) * sa;
+    sl.y(npk) = (pos_x - pos_x) * sa + (pos_y - pos_y) * ca;
     int ncp = 1;
     double cps = dist;
     for (int i = 0; i < 5; i++) {
@@ -318,19 +327,19 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
         total += sqrt((npx - lx) * (npx - lx) + (npy - ly) * (npy - ly));
         lx = npx; ly = npy;
         const double tx0 = npx - pos_x, ty0 = npy - pos_y;
-        sl.X[npk + ncp] = tx0 * ca - ty0 * sa;
-        sl.Y[npk + ncp] = tx0 * sa + ty0 * ca;
+        sl.x(npk + ncp) = tx0 * ca - ty0 * sa;
+        sl.y(npk + ncp) = tx0 * sa + ty0 * ca;
         ncp++;
         if (total > 50 && ncp > 2) break;
         cps += min_cpd;
     }
     int nk = npk + ncp;
     for (int i = 1; i < nk; i++) {                                      // :833-843
-        if (sl.X[i] <= sl.X[i - 1]) { nk = i; flags |= kMetaTrunc; break; }
+        if (sl.x(i) <= sl.x(i - 1)) { nk = i; flags |= kMetaTrunc; break; }
     }
     const bool fallback = nk < 3 || nk <= npk || fabs(ego_d) > 20;      // :848
     if (fallback) flags |= kMetaFallback;
-    sl.meta[0] = nk; sl.meta[1] = ncp; sl.meta[2] = npk; sl.meta[3] = flags;
+    sl.m(0) = nk; sl.m(1) = ncp; sl.m(2) = npk; sl.m(3) = flags;
     if (fallback) return;
     // tk::spline::set_points (spline.h:284-373): tridiagonal band LU, rows preconditioned,
     // no pivoting. Forward sweep fuses preconditioning, Gauss step and l_solve row by row
@@ -343,8 +352,8 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
         if (i == 0) { dg = 2.0; up = 0.0; r = 0.0; }
         else if (i == n - 1) { dg = 2.0; lo = 0.0; r = 0.0; }
         else {
-            const double xm = sl.X[i - 1], x0 = sl.X[i], xp = sl.X[i + 1];
-            const double ym = sl.Y[i - 1], y0 = sl.Y[i], yp = sl.Y[i + 1];
+            const double xm = sl.x(i - 1), x0 = sl.x(i), xp = sl.x(i + 1);
+            const double ym = sl.y(i - 1), y0 = sl.y(i), yp = sl.y(i + 1);
             lo = 1.0 / 3.0 * (x0 - xm);
             dg = 2.0 / 3.0 * (xp - xm);
             up = 1.0 / 3.0 * (xp - x0);
@@ -362,25 +371,25 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
             sum += lo * yy_prev;                                        // l_solve
         }
         const double yy = (r * sd) - sum;
-        sl.A[i] = up; sl.C[i] = dg; sl.B[i] = yy;
+        sl.a(i) = up; sl.c(i) = dg; sl.b(i) = yy;
         up_prev = up; dg_prev = dg; yy_prev = yy;
     }
     double bb_next = 0;
     for (int i = n - 1; i >= 0; i--) {                                  // r_solve
         double sum = 0;
-        if (i < n - 1) sum += sl.A[i] * bb_next;
-        const double bb = (sl.B[i] - sum) / sl.C[i];
-        sl.B[i] = bb;
+        if (i < n - 1) sum += sl.a(i) * bb_next;
+        const double bb = (sl.b(i) - sum) / sl.c(i);
+        sl.b(i) = bb;
         bb_next = bb;
     }
     for (int i = 0; i < n - 1; i++) {                                   // spline.h:345-349
-        const double dx = sl.X[i + 1] - sl.X[i];
-        sl.A[i] = 1.0 / 3.0 * (sl.B[i + 1] - sl.B[i]) / dx;
-        sl.C[i] = (sl.Y[i + 1] - sl.Y[i]) / dx - 1.0 / 3.0 * (2.0 * sl.B[i] + sl.B[i + 1]) * dx;
+        const double dx = sl.x(i + 1) - sl.x(i);
+        sl.a(i) = 1.0 / 3.0 * (sl.b(i + 1) - sl.b(i)) / dx;
+        sl.c(i) = (sl.y(i + 1) - sl.y(i)) / dx - 1.0 / 3.0 * (2.0 * sl.b(i) + sl.b(i + 1)) * dx;
     }
-    const double h = sl.X[n - 1] - sl.X[n - 2];                         // spline.h:367-370
-    sl.A[n - 1] = 0.0;
-    sl.C[n - 1] = 3.0 * sl.A[n - 2] * h * h + 2.0 * sl.B[n - 2] * h + sl.C[n - 2];
+    const double h = sl.x(n - 1) - sl.x(n - 2);                         // spline.h:367-370
+    sl.a(n - 1) = 0.0;
+    sl.c(n - 1) = 3.0 * sl.a(n - 2) * h * h + 2.0 * sl.b(n - 2) * h + sl.c(n - 2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -388,15 +397,20 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
 // ------------------------------------------------------------------------------------------------
 struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; };
 
-// Output targets: point g (0-based among generated) goes to wx[g*ws], wy[g*ws] (if wx) and
-// px[g*ps], px[g*ps+1] (if px).
-template <bool kLarge>
-__device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double cy, double angle,
-                                 double ca0, double sa0, SC sc, int room, double* wx, double* wy,
-                                 int64_t ws, double* px, int64_t ps) {
+// kOut = false: cost only. The curvature adjustment (src/main.cpp:972-1018) rotates only the
+// local->global transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that
+// the cost reads never depends on it, so the cost-only loop skips the transform, its sin/cos and
+// the output stores. kOut = true also produces the points: point g goes to wx[g*ws], wy[g*ws]
+// (if wx) and px[g*ps], px[g*ps+1] (if px).
+// kCache: keep the current spline segment (bounds + coefficients) in registers; the segment
+// changes every ~10-40 steps, so most steps read no slot memory.
+template <bool kLarge, bool kOut, bool kCache>
+__device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
+                                 double angle, double ca0, double sa0, SC sc, int room, double* wx,
+                                 double* wy, int64_t ws, double* px, int64_t ps) {
     CandRes R;
     R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0;
-    const int nk = sl.meta[0], ncp = sl.meta[1], npk = sl.meta[2], mflags = sl.meta[3];
+    const int nk = sl.m(0), ncp = sl.m(1), npk = sl.m(2), mflags = sl.m(3);
     if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
     double pos_x = 0, pos_y = 0;
@@ -410,7 +424,7 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
         int nc = 1;
         while (ng < room && nc < ncp) {
             const double dstep = speed / 50;
-            const double ndx = sl.X[npk + nc] - pos_x, ndy = sl.Y[npk + nc] - pos_y;
+            const double ndx = sl.x(npk + nc) - pos_x, ndy = sl.y(npk + nc) - pos_y;
             const double cpd = sqrt(ndx * ndx + ndy * ndy);
             if (cpd < 5) { nc++; continue; }
             cur_t += 0.02;
@@ -428,10 +442,12 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
             ppm::sincos_pp<kLarge>(cang, sc_, cc_);
             pos_x += cc_ * dstep;
             pos_y += sc_ * dstep;
-            const double tx = pos_x * ca - pos_y * sa;
-            const double ty = pos_x * sa + pos_y * ca;
-            if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-            if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+            if (kOut) {
+                const double tx = pos_x * ca - pos_y * sa;
+                const double ty = pos_x * sa + pos_y * ca;
+                if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+                if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+            }
             ng++;
             R.travelled += dstep;
         }
@@ -439,20 +455,27 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
         return R;
     }
     int cnt = 0;                     // #knots with X < x (std::lower_bound position)
+    // cached segment: valid while seg_lo < x <= seg_hi (NaN x never valid)
+    double seg_lo = 1.0, seg_hi = 0.0, sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
     double arg = 0, prev_speed = sc.start, prev_angle = 0;
     while (arg < 50 && ng < room) {
         double speed = sc_get_speed(sc, cur_t);
         double dstep = speed / 50;
         const double x = arg + dstep;
         // tk::spline::operator() (spline.h:375-396)
-        while (cnt < nk && sl.X[cnt] < x) cnt++;
-        while (cnt > 0 && !(sl.X[cnt - 1] < x)) cnt--;
-        const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
-        const double h = x - sl.X[idx];
+        if (!kCache || !(seg_lo < x && x <= seg_hi)) {
+            while (cnt < nk && sl.x(cnt) < x) cnt++;
+            while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
+            const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+            seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
+            seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
+            sx = sl.x(idx); sa_ = sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+        }
+        const double h = x - sx;
         double y;
-        if (cnt == 0 && x < sl.X[0]) y = (sl.B[0] * h + sl.C[0]) * h + sl.Y[0];          // left
-        else if (cnt == nk && x > sl.X[nk - 1]) y = (sl.B[idx] * h + sl.C[idx]) * h + sl.Y[idx];  // right
-        else y = ((sl.A[idx] * h + sl.B[idx]) * h + sl.C[idx]) * h + sl.Y[idx];
+        if (cnt == 0 && x < sx) y = (sb * h + sc_) * h + sy;                       // left
+        else if (cnt == nk && x > sx) y = (sb * h + sc_) * h + sy;                 // right
+        else y = ((sa_ * h + sb) * h + sc_) * h + sy;
         const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
         double acc = fabs(speed - prev_speed) * 50;
         const double astep = ppm::atan2_pp(y - pos_y, x - pos_x);
@@ -474,22 +497,24 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
                 double nc = P.maximum_acc - acc;
                 if (nc < 0) nc = 0;
-                double nad = nc / speed / 50;
-                if (adiff < 0) nad *= -1;
-                const double rot = nad - adiff;
-                double tpx = pos_x * ca - pos_y * sa;
-                double tpy = pos_x * sa + pos_y * ca;
-                tpx = tpx + cx;
-                tpy = tpy + cy;
-                const double vx = cx - tpx, vy = cy - tpy;
-                double cr, sr;
-                ppm::sincos_pp<kLarge>(rot, sr, cr);
-                const double rvx = vx * cr - vy * sr;
-                const double rvy = vx * sr + vy * cr;
-                cx = tpx + rvx;
-                cy = tpy + rvy;
-                tangle += rot;
-                ppm::sincos_pp<kLarge>(tangle, sa, ca);
+                if (kOut) {
+                    double nad = nc / speed / 50;
+                    if (adiff < 0) nad *= -1;
+                    const double rot = nad - adiff;
+                    double tpx = pos_x * ca - pos_y * sa;
+                    double tpy = pos_x * sa + pos_y * ca;
+                    tpx = tpx + cx;
+                    tpy = tpy + cy;
+                    const double vx = cx - tpx, vy = cy - tpy;
+                    double cr, sr;
+                    ppm::sincos_pp<kLarge>(rot, sr, cr);
+                    const double rvx = vx * cr - vy * sr;
+                    const double rvy = vx * sr + vy * cr;
+                    cx = tpx + rvx;
+                    cy = tpy + rvy;
+                    tangle += rot;
+                    ppm::sincos_pp<kLarge>(tangle, sa, ca);
+                }
                 eff_c = nc;
                 R.flags |= PP_ST_CURV_ADJUST;
             }
@@ -501,10 +526,12 @@ __device__ CandRes run_candidate(const pp_params& P, Slot sl, double cx, double 
         pos_y += (y - pos_y) * dstep / d;
         arg += sp_step;
         pos_x += sp_step;
-        const double tx = pos_x * ca - pos_y * sa;
-        const double ty = pos_x * sa + pos_y * ca;
-        if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-        if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+        if (kOut) {
+            const double tx = pos_x * ca - pos_y * sa;
+            const double ty = pos_x * sa + pos_y * ca;
+            if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+            if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+        }
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -546,12 +573,17 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
     return sc;
 }
 
+#ifndef PP_CAND_CACHE
+#define PP_CAND_CACHE 1
+#endif
+
 // ------------------------------------------------------------------------------------------------
-// K2: candidates
-// ------------------------------------------------------------------------------------------------
+// K2: candidates. One workgroup = SPB scenes x C candidates; slots in LDS.
 // kSlow = false: every scene except those flagged kLimSlow by k_prep (no library call in the
 // loop, so the register peak stays at the loop's own state); kSlow = true: only flagged scenes.
-template <bool kSlow>
+// kPaths: every candidate writes its path (emit_paths); otherwise cost only.
+// ------------------------------------------------------------------------------------------------
+template <bool kSlow, bool kPaths>
 __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -576,7 +608,7 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
     if (tid < SPB) sFlags[tid] = 0;
     if (tid < 3 * nsc && (((pv.lim_mask[s0 + tid / 3] & kLimSlow) != 0) == kSlow)) {   // phase A
         const int j = tid;
-        Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j};
+        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         setup_lane(m, P, in, pv, s0 + j / 3, j % 3, sl);
     }
     __syncthreads();
@@ -585,44 +617,32 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
         const int64_t s = s0 + sc_l;
         const int L = c / NS, k = c - L * NS;
         const int j = sc_l * 3 + L;
-        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j};
+        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         const double v = cand_speed(P, pv.ego_speed[s], k);
         const SC sc = make_sc(P, pv, S, s, L, v);
         const int K = pv.K[s], T = pv.T[s];
-        const bool winner = P.cost_mode == PP_COST_REFERENCE && L == T && k == 0;
-        double* wx = nullptr; double* wy = nullptr;
-        double* px = nullptr;
-        const int64_t ps = (int64_t)C * 2;
-        if (winner) {
-            wx = out.next_x + s * N + K; wy = out.next_y + s * N + K;
-            for (int i = 0; i < K; i++) {
-                out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
-                out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
-            }
-        }
-        if (P.emit_paths && out.paths) {
-            px = out.paths + ((s * N + K) * C + c) * 2;
+        CandRes R;
+        if (kPaths) {
+            const int64_t ps = (int64_t)C * 2;
             double* p0 = out.paths + ((s * N) * C + c) * 2;
             for (int i = 0; i < K; i++) {
                 p0[i * ps] = in.prev_x[(int64_t)i * S + s];
                 p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
             }
+            double* px = p0 + K * ps;
+            R = run_candidate<kSlow, true, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
+                                                          pv.ca_p[s], pv.sa_p[s], sc, N - K,
+                                                          nullptr, nullptr, 0, px, ps);
+            for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
+            if (out.path_len) out.path_len[s * C + c] = K + R.ng;
+        } else {
+            R = run_candidate<kSlow, false, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
+                                                           nullptr, nullptr, 0, nullptr, 0);
         }
-        const CandRes R = run_candidate<kSlow>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
-                                               pv.sa_p[s], sc, N - K, wx, wy, 1, px, ps);
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
                                       pv.ego_lane[s], flags);
         out.cost[s * C + c] = cost;
-        if (winner) {
-            for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
-            out.n_out[s] = K + R.ng;
-            out.winner[s] = c;
-        }
-        if (px) {
-            for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
-        }
-        if (P.emit_paths && out.path_len) out.path_len[s * C + c] = K + R.ng;
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
@@ -631,17 +651,19 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3: comfort-mode winner (argmin + re-run), one lane per scene, private LDS slot per lane
+// K3: per-scene winner: argmin over the candidate costs (first minimum, as the oracle), then the
+// winning candidate re-run with outputs -> next_x/next_y (prev points + generated points).
+// One lane per scene; the winner's spline lives in a global scratch [field][knot][S].
 // ------------------------------------------------------------------------------------------------
-constexpr int kWinBlock = 64;
+constexpr int kWinBlock = 256;
+template <bool kSlow>
 __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in, pp_params P,
-                                                      PrepV pv, pp_result out) {
-    __shared__ __attribute__((aligned(16))) double wsm[5 * kWinBlock * kKP];
-    __shared__ int wmeta[4 * kWinBlock];
+                                                      PrepV pv, pp_result out, double* spl) {
     const MapV m = map_view(mg.buf, mg.n);
     const int64_t S = in.n_scenes;
     const int64_t s = (int64_t)blockIdx.x * kWinBlock + threadIdx.x;
     if (s >= S) return;
+    if (((pv.lim_mask[s] & kLimSlow) != 0) != kSlow) return;
     const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
     int best = 0;
     double bc = out.cost[s * C];
@@ -650,10 +672,9 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         if (v < bc) { bc = v; best = c; }
     }
     const int L = best / NS, k = best - L * NS;
-    const int j = threadIdx.x;
-    const Slot sl = {wsm + (0 * kWinBlock + j) * kKP, wsm + (1 * kWinBlock + j) * kKP,
-                     wsm + (2 * kWinBlock + j) * kKP, wsm + (3 * kWinBlock + j) * kKP,
-                     wsm + (4 * kWinBlock + j) * kKP, wmeta + 4 * j};
+    const int64_t KS = (int64_t)PP_MAX_KNOTS * S;
+    const Slot sl = {spl + s, spl + KS + s, spl + 2 * KS + s, spl + 3 * KS + s, spl + 4 * KS + s,
+                     (int*)(spl + 5 * KS) + s, S};
     setup_lane(m, P, in, pv, s, L, sl);
     const double v = cand_speed(P, pv.ego_speed[s], k);
     const SC sc = make_sc(P, pv, S, s, L, v);
@@ -662,9 +683,10 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
         out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
     }
-    const CandRes R = run_candidate<true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s], pv.ca_p[s],
-                                    pv.sa_p[s], sc, N - K, out.next_x + s * N + K,
-                                    out.next_y + s * N + K, 1, nullptr, 0);
+    const CandRes R = run_candidate<kSlow, true, true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
+                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K,
+                                                       out.next_x + s * N + K, out.next_y + s * N + K,
+                                                       1, nullptr, 0);
     for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
     out.n_out[s] = K + R.ng;
     out.winner[s] = best;
@@ -798,7 +820,10 @@ int dev_init(pp_map* M, int device) {
     return PP_OK;
 }
 
-size_t prep_bytes(int64_t S) { return (size_t)S * (kPrepD * 8 + kPrepI * 4) + 256; }
+size_t prep_bytes(int64_t S) { return ((size_t)S * (kPrepD * 8 + kPrepI * 4) + 255) / 256 * 256; }
+// k_winner spline scratch: 5 double arrays [PP_MAX_KNOTS][S] + 4 int arrays [S]
+size_t spline_bytes(int64_t S) { return (size_t)S * (5 * PP_MAX_KNOTS * 8 + 4 * 4) + 256; }
+double* spline_scratch(void* ws, int64_t cap) { return (double*)((char*)ws + prep_bytes(cap)); }
 
 PrepV prep_bind(void* base, int64_t S) {
     PrepV p;
@@ -823,7 +848,7 @@ int ensure_ws(pp_map* M, int device, int64_t S) {
     DevState& D = M->dev[device];
     if (D.ws_cap >= S) return PP_OK;
     if (D.ws) { (void)hipDeviceSynchronize(); (void)hipFree(D.ws); D.ws = nullptr; D.ws_cap = 0; }
-    if (hipMalloc(&D.ws, prep_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMalloc(&D.ws, prep_bytes(S) + spline_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
     D.ws_cap = S;
     return PP_OK;
 }
@@ -927,6 +952,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const int64_t S = in->n_scenes;
     PrepV pv;
     MapG mg;
+    double* spl = nullptr;
     {
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
@@ -934,6 +960,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         rc = ensure_ws(M, device, S);
         if (rc) return rc;
         pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
+        spl = spline_scratch(M->dev[device].ws, M->dev[device].ws_cap);
         mg.buf = M->dev[device].map;
         mg.n = M->n;
     }
@@ -954,7 +981,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 D.ev_pool.pop_back();
                 D.ev_rec.push_back(ev[i]);
             }
-            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT ? 1 : 0);
+            D.ev_has3.push_back(1);
         }
     }
     pp_params P = *prm;
@@ -978,14 +1005,21 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
         const int64_t blocks = (S + spb - 1) / spb;
         if (timing) (void)hipEventRecord(ev[1], st);
-        hipLaunchKernelGGL(k_cand<false>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-        hipLaunchKernelGGL(k_cand<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        if (P.emit_paths) {
+            hipLaunchKernelGGL((k_cand<false, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        } else {
+            hipLaunchKernelGGL((k_cand<false, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        }
     }
     if (timing) (void)hipEventRecord(ev[2], st);
-    // K3 (comfort mode)
-    if (P.cost_mode == PP_COST_COMFORT) {
+    // K3: argmin + winner path (every mode); the spline scratch is sized to ws_cap
+    {
+        // the scratch layout uses the batch size as its stride: bind it to S (<= ws_cap)
         const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
-        hipLaunchKernelGGL(k_winner, dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+        hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);
+        hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);
     }
     if (timing) (void)hipEventRecord(ev[3], st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;

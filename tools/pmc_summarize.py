@@ -16,7 +16,7 @@ tag = sys.argv[2] if len(sys.argv) > 2 else None
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        k = row.get("Kernel_Name", "").split("(")[0]
+        k = row.get("Kernel_Name", "").split("(")[0].replace("void ", "").strip()
         vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 summary = {}
 for k, d in vals.items():
@@ -24,7 +24,7 @@ for k, d in vals.items():
     summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
 print(json.dumps(summary, indent=1))
 if tag:
-    kc = summary.get("k_cand", {})
+    kc = summary.get("k_cand<false>", summary.get("k_cand", {}))
     out = {}
     p = "profiles/pmc_summary.json"
     if os.path.exists(p):
