@@ -10,7 +10,8 @@
 //                Phase B: one lane per candidate runs the 0.02 s resampling loop with the
 //                accel/curvature limiter (src/main.cpp:905-1041) reading its spline from LDS
 //                and computes the candidate cost (cost-only loop unless every path is emitted).
-//   K3 k_winner  per-scene argmin + re-run of the winning candidate with outputs (next_x/next_y).
+//   K3 k_winner  comfort mode: per-scene argmin + re-run of the winning candidate with outputs.
+//                (reference mode: the winner is known before the loop; its k_cand lane writes them)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -397,17 +398,19 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
 // ------------------------------------------------------------------------------------------------
 struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; };
 
-// kOut = false: cost only. The curvature adjustment (src/main.cpp:972-1018) rotates only the
-// local->global transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that
-// the cost reads never depends on it, so the cost-only loop skips the transform, its sin/cos and
-// the output stores. kOut = true also produces the points: point g goes to wx[g*ws], wy[g*ws]
-// (if wx) and px[g*ps], px[g*ps+1] (if px).
+// Output modes. The curvature adjustment (src/main.cpp:972-1018) rotates only the local->global
+// transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that the cost reads
+// never depends on it, so a cost-only lane skips the transform, its sin/cos and the stores.
+//   kOutMode 0: cost only;  2: every lane produces points;  1: lanes with out_on produce points
+//   (reference mode: the winner lane of each scene, known before the loop).
+// Point g goes to wx[g*ws], wy[g*ws] (if wx) and px[g*ps], px[g*ps+1] (if px).
 // kCache: keep the current spline segment (bounds + coefficients) in registers; the segment
 // changes every ~10-40 steps, so most steps read no slot memory.
-template <bool kLarge, bool kOut, bool kCache>
+template <bool kLarge, int kOutMode, bool kCache>
 __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
                                  double angle, double ca0, double sa0, SC sc, int room, double* wx,
-                                 double* wy, int64_t ws, double* px, int64_t ps) {
+                                 double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true) {
+    const bool kOut = kOutMode == 2 || (kOutMode == 1 && out_on);
     CandRes R;
     R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0;
     const int nk = sl.m(0), ncp = sl.m(1), npk = sl.m(2), mflags = sl.m(3);
@@ -442,7 +445,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             ppm::sincos_pp<kLarge>(cang, sc_, cc_);
             pos_x += cc_ * dstep;
             pos_y += sc_ * dstep;
-            if (kOut) {
+            if (kOutMode != 0 && kOut) {
                 const double tx = pos_x * ca - pos_y * sa;
                 const double ty = pos_x * sa + pos_y * ca;
                 if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
@@ -497,7 +500,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
                 double nc = P.maximum_acc - acc;
                 if (nc < 0) nc = 0;
-                if (kOut) {
+                if (kOutMode != 0 && kOut) {
                     double nad = nc / speed / 50;
                     if (adiff < 0) nad *= -1;
                     const double rot = nad - adiff;
@@ -526,7 +529,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         pos_y += (y - pos_y) * dstep / d;
         arg += sp_step;
         pos_x += sp_step;
-        if (kOut) {
+        if (kOutMode != 0 && kOut) {
             const double tx = pos_x * ca - pos_y * sa;
             const double ty = pos_x * sa + pos_y * ca;
             if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
@@ -581,10 +584,14 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 // K2: candidates. One workgroup = SPB scenes x C candidates; slots in LDS.
 // kSlow = false: every scene except those flagged kLimSlow by k_prep (no library call in the
 // loop, so the register peak stays at the loop's own state); kSlow = true: only flagged scenes.
-// kPaths: every candidate writes its path (emit_paths); otherwise cost only.
+// kMode 2: every candidate writes its path (emit_paths); 1: reference mode, the winner lanes
+// write next_x/next_y; 0: cost only (comfort mode; k_winner produces the outputs).
 // ------------------------------------------------------------------------------------------------
-template <bool kSlow, bool kPaths>
-__global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+#ifndef PP_CAND_WAVES
+#define PP_CAND_WAVES 4
+#endif
+template <bool kSlow, int kMode>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
@@ -621,8 +628,21 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
         const double v = cand_speed(P, pv.ego_speed[s], k);
         const SC sc = make_sc(P, pv, S, s, L, v);
         const int K = pv.K[s], T = pv.T[s];
+        // reference mode: the winning candidate (planner lane, max_speed) is known before the
+        // loop, so its lane writes next_x/next_y (point-major) during the same pass
+        const bool winner = kMode != 0 && P.cost_mode == PP_COST_REFERENCE && L == T && k == 0;
+        double* wx = nullptr;
+        double* wy = nullptr;
+        if (winner) {
+            for (int i = 0; i < K; i++) {
+                out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+                out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+            }
+            wx = out.next_x + (int64_t)K * S + s;
+            wy = out.next_y + (int64_t)K * S + s;
+        }
         CandRes R;
-        if (kPaths) {
+        if (kMode == 2) {
             const int64_t ps = (int64_t)C * 2;
             double* p0 = out.paths + ((s * N) * C + c) * 2;
             for (int i = 0; i < K; i++) {
@@ -630,14 +650,23 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
                 p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
             }
             double* px = p0 + K * ps;
-            R = run_candidate<kSlow, true, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
-                                                          pv.ca_p[s], pv.sa_p[s], sc, N - K,
-                                                          nullptr, nullptr, 0, px, ps);
+            R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
+                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K, wx, wy, S,
+                                                       px, ps);
             for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
             if (out.path_len) out.path_len[s * C + c] = K + R.ng;
+        } else if (kMode == 1) {
+            R = run_candidate<kSlow, 1, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
+                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K, wx, wy, S,
+                                                       nullptr, 0, winner);
         } else {
-            R = run_candidate<kSlow, false, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
-                                                           nullptr, nullptr, 0, nullptr, 0);
+            R = run_candidate<kSlow, 0, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
+                                                       nullptr, nullptr, 0, nullptr, 0);
+        }
+        if (winner) {
+            for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
+            out.n_out[s] = K + R.ng;
+            out.winner[s] = c;
         }
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
@@ -651,9 +680,9 @@ __global__ __launch_bounds__(256) void k_cand(MapG mg, pp_scene_batch in, pp_par
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3: per-scene winner: argmin over the candidate costs (first minimum, as the oracle), then the
-// winning candidate re-run with outputs -> next_x/next_y (prev points + generated points).
-// One lane per scene; the winner's spline lives in a global scratch [field][knot][S].
+// K3 (comfort mode): per-scene argmin over the candidate costs (first minimum, as the oracle), then
+// the winning candidate re-run with outputs. One lane per scene; next_x/next_y are point-major
+// ([i * S + s], the batch's own convention), so every step of a wave stores 512 contiguous bytes.
 // ------------------------------------------------------------------------------------------------
 constexpr int kWinBlock = 256;
 template <bool kSlow>
@@ -662,8 +691,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     const MapV m = map_view(mg.buf, mg.n);
     const int64_t S = in.n_scenes;
     const int64_t s = (int64_t)blockIdx.x * kWinBlock + threadIdx.x;
-    if (s >= S) return;
-    if (((pv.lim_mask[s] & kLimSlow) != 0) != kSlow) return;
+    if (s >= S || ((pv.lim_mask[s] & kLimSlow) != 0) != kSlow) return;
     const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
     int best = 0;
     double bc = out.cost[s * C];
@@ -672,6 +700,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         if (v < bc) { bc = v; best = c; }
     }
     const int L = best / NS, k = best - L * NS;
+    // strided scratch [field][knot][S]: a wave's accesses to one knot are 512 contiguous bytes
     const int64_t KS = (int64_t)PP_MAX_KNOTS * S;
     const Slot sl = {spl + s, spl + KS + s, spl + 2 * KS + s, spl + 3 * KS + s, spl + 4 * KS + s,
                      (int*)(spl + 5 * KS) + s, S};
@@ -680,14 +709,14 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     const SC sc = make_sc(P, pv, S, s, L, v);
     const int K = pv.K[s];
     for (int i = 0; i < K; i++) {
-        out.next_x[s * N + i] = in.prev_x[(int64_t)i * S + s];
-        out.next_y[s * N + i] = in.prev_y[(int64_t)i * S + s];
+        out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+        out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
     }
-    const CandRes R = run_candidate<kSlow, true, true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
-                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K,
-                                                       out.next_x + s * N + K, out.next_y + s * N + K,
-                                                       1, nullptr, 0);
-    for (int i = K + R.ng; i < N; i++) { out.next_x[s * N + i] = 0; out.next_y[s * N + i] = 0; }
+    const CandRes R = run_candidate<kSlow, 2, true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
+                                                    pv.ca_p[s], pv.sa_p[s], sc, N - K,
+                                                    out.next_x + (int64_t)K * S + s,
+                                                    out.next_y + (int64_t)K * S + s, S, nullptr, 0);
+    for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
     out.n_out[s] = K + R.ng;
     out.winner[s] = best;
 }
@@ -821,7 +850,7 @@ int dev_init(pp_map* M, int device) {
 }
 
 size_t prep_bytes(int64_t S) { return ((size_t)S * (kPrepD * 8 + kPrepI * 4) + 255) / 256 * 256; }
-// k_winner spline scratch: 5 double arrays [PP_MAX_KNOTS][S] + 4 int arrays [S]
+// k_winner scratch: 5 double arrays [PP_MAX_KNOTS][S] + 4 int arrays [S]
 size_t spline_bytes(int64_t S) { return (size_t)S * (5 * PP_MAX_KNOTS * 8 + 4 * 4) + 256; }
 double* spline_scratch(void* ws, int64_t cap) { return (double*)((char*)ws + prep_bytes(cap)); }
 
@@ -981,7 +1010,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 D.ev_pool.pop_back();
                 D.ev_rec.push_back(ev[i]);
             }
-            D.ev_has3.push_back(1);
+            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT ? 1 : 0);
         }
     }
     pp_params P = *prm;
@@ -1006,17 +1035,19 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const int64_t blocks = (S + spb - 1) / spb;
         if (timing) (void)hipEventRecord(ev[1], st);
         if (P.emit_paths) {
-            hipLaunchKernelGGL((k_cand<false, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-            hipLaunchKernelGGL((k_cand<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+        } else if (P.cost_mode == PP_COST_REFERENCE) {
+            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
         } else {
-            hipLaunchKernelGGL((k_cand<false, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-            hipLaunchKernelGGL((k_cand<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
         }
     }
     if (timing) (void)hipEventRecord(ev[2], st);
-    // K3: argmin + winner path (every mode); the spline scratch is sized to ws_cap
-    {
-        // the scratch layout uses the batch size as its stride: bind it to S (<= ws_cap)
+    // K3 (comfort mode): argmin + winner path; scratch regions are sized to ws_cap >= S
+    if (P.cost_mode == PP_COST_COMFORT) {
         const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
         hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);
         hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);

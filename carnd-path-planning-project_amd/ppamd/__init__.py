@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libppamd.so")
+LIB_PATH = os.environ.get("PPAMD_LIB") or os.path.join(_HERE, "libppamd.so")   # override: A/B builds
 
 NUM_LANES = 3
 PREV_KEEP = 10
@@ -269,8 +269,9 @@ def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
         import torch
         mk = lambda sh, dt: torch.zeros(sh, dtype=dt, device=device)
         f8, i4, u4 = torch.float64, torch.int32, torch.int32
-    r = {"winner": mk((S,), i4), "n_out": mk((S,), i4), "next_x": mk((S, N), f8),
-         "next_y": mk((S, N), f8), "cost": mk((S, Cn), f8), "status": mk((S,), u4)}
+    # next_x/next_y are point-major [N][S] (include/pp.h)
+    r = {"winner": mk((S,), i4), "n_out": mk((S,), i4), "next_x": mk((N, S), f8),
+         "next_y": mk((N, S), f8), "cost": mk((S, Cn), f8), "status": mk((S,), u4)}
     if prm.emit_paths:
         r["paths"] = mk((S, N, Cn, 2), f8)
         r["path_len"] = mk((S, Cn), i4)

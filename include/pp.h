@@ -127,7 +127,8 @@ typedef struct pp_scene_info {
 
 /* ---- results (caller owned; device resident for pp_eval) ---------------------------------- */
 /* C = PP_NUM_LANES * n_speeds, candidate c = lane * n_speeds + k.
- * next_x/next_y: [s * n_points + i]; cost: [s * C + c];
+ * next_x/next_y: point-major like the batch's prev_x/prev_y, [i * n_scenes + s] (i < n_points;
+ * points i >= n_out[s] are 0); cost: [s * C + c];
  * paths (emit_paths): [((s * n_points + i) * C + c) * 2 + {0:x, 1:y}], path_len: [s * C + c]. */
 typedef struct pp_result {
     int32_t*  winner;

@@ -929,8 +929,8 @@ int ppo_eval_range(const double* wx, const double* wy, int n_wp, const pp_scene_
                     double px = 0, py = 0;
                     if (i < pr.K) { px = pr.prev[i].x; py = pr.prev[i].y; }
                     else if (i - pr.K < ng) { px = gx[i - pr.K]; py = gy[i - pr.K]; }
-                    out->next_x[s * N + i] = px;
-                    out->next_y[s * N + i] = py;
+                    out->next_x[(int64_t)i * in->n_scenes + s] = px;
+                    out->next_y[(int64_t)i * in->n_scenes + s] = py;
                 }
             }
         }

@@ -177,7 +177,7 @@ def main():
     T = ref["ref_T"]
     assert (ores["info"]["target_lane"] == T).all()
     assert (ores["winner"] == T * N_SPEEDS).all()
-    wn = np.stack([ores["next_x"], ores["next_y"]], -1)
+    wn = np.stack([ores["next_x"].T, ores["next_y"].T], -1)   # next_x is point-major [N][S]
     assert (wn == ref["ref_next"]).all() and (ores["n_out"] == ref["ref_n"]).all()
     np.savez_compressed(
         os.path.join(HERE, "golden_scenes.npz"),

@@ -85,11 +85,11 @@ def compare(got, ref, check_cost=True):
     # winners: exact, except comfort-mode scenes whose costs include a quirk candidate
     win_quirk = quirk[np.arange(S), np.clip(ref["winner"], 0, Cn - 1)] | quirk[np.arange(S), np.clip(got["winner"], 0, Cn - 1)]
     assert (got["winner"][~qs] == ref["winner"][~qs]).all()
-    N = got["next_x"].shape[1]
+    N = got["next_x"].shape[0]          # next_x/next_y are point-major [N][S]
     idx = np.arange(N)
     for s in range(S):
-        gn = np.stack([got["next_x"][s], got["next_y"][s]], -1)
-        rn = np.stack([ref["next_x"][s], ref["next_y"][s]], -1)
+        gn = np.stack([got["next_x"][:, s], got["next_y"][:, s]], -1)
+        rn = np.stack([ref["next_x"][:, s], ref["next_y"][:, s]], -1)
         if win_quirk[s] or (qs[s] and got["winner"][s] != ref["winner"][s]):
             continue
         assert got["n_out"][s] == ref["n_out"][s], s
@@ -121,7 +121,7 @@ def test_golden_reference_vectors(env):
     assert (got["path_len"] == G["ref_path_len"]).all()
     assert (got["winner"] == G["ref_T"] * int(G["n_speeds"])).all()
     assert (got["n_out"] == G["ref_n"]).all()
-    e2 = max_err(np.stack([got["next_x"], got["next_y"]], -1), G["ref_next"])
+    e2 = max_err(np.stack([got["next_x"].T, got["next_y"].T], -1), G["ref_next"])
     assert e2 <= TOL, e2
     assert (got["info"]["target_lane"] == G["ref_T"]).all()
     np.testing.assert_allclose(got["cost"], G["oracle_cost"], rtol=1e-9, atol=1e-9)
@@ -233,8 +233,10 @@ def test_full_size_properties(env):
     r3 = ppamd.alloc_result(hi - lo, prm, xp="torch", device=env["dev"])
     ppamd.evaluate(env["m"], sub, prm, r3, device=0)
     torch.cuda.synchronize()
-    for k in ("winner", "n_out", "next_x", "next_y", "cost", "status"):
+    for k in ("winner", "n_out", "cost", "status"):
         assert torch.equal(r1[k][lo:hi], r3[k]), k
+    for k in ("next_x", "next_y"):
+        assert torch.equal(r1[k][:, lo:hi], r3[k]), k
     info = r1["info"].cpu().numpy().view(ppamd.INFO_DTYPE).reshape(-1)
     assert torch.equal(r1["winner"].cpu(), torch.from_numpy(info["target_lane"] * 5))
     cost = r1["cost"]
@@ -245,5 +247,6 @@ def test_full_size_properties(env):
     idx = np.arange(0, S, S // 512)
     host = {k: np.ascontiguousarray(v.cpu().numpy()[..., idx]) for k, v in scenes.items()}
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], host, prm, info=False)
-    got = {k: v[idx] for k, v in ppamd.result_to_numpy({k: r1[k] for k in ("winner", "n_out", "next_x", "next_y", "cost", "status")}).items()}
+    got = {k: (v[:, idx] if k.startswith("next") else v[idx])
+           for k, v in ppamd.result_to_numpy({k: r1[k] for k in ("winner", "n_out", "next_x", "next_y", "cost", "status")}).items()}
     compare(got, ref)

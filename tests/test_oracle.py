@@ -58,7 +58,7 @@ def test_oracle_frame_trajectory_is_reference_choice(olib):
     assert (r["info"]["target_lane"] == G["ref_T"]).all()
     assert (r["winner"] == G["ref_T"] * ns).all()
     assert (r["n_out"] == G["ref_n"]).all()
-    assert np.array_equal(np.stack([r["next_x"], r["next_y"]], -1), G["ref_next"])
+    assert np.array_equal(np.stack([r["next_x"].T, r["next_y"].T], -1), G["ref_next"])
     info = G["ref_info"]
     assert np.array_equal(r["info"]["ego_s"], info[:, 0])
     assert np.array_equal(r["info"]["ego_d"], info[:, 1])
@@ -94,4 +94,4 @@ def test_oracle_vs_reference_large_pool(olib):
         o = oracle_lib.oracle_eval(olib, wx, wy, sc, prm)
         op = np.transpose(o["paths"], (0, 2, 1, 3))
         assert ((op == ref["paths"]) | (np.isnan(op) & np.isnan(ref["paths"]))).all()
-        assert np.array_equal(np.stack([o["next_x"], o["next_y"]], -1), ref["ref_next"])
+        assert np.array_equal(np.stack([o["next_x"].T, o["next_y"].T], -1), ref["ref_next"])
