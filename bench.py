@@ -33,6 +33,22 @@ def algorithmic_bytes_per_candidate(C_, N, emit_paths):
     return (SCENE_BYTES + 8 + 16 * N) / C_ + 8
 
 
+def shard(rank, scenes_per_rank):
+    """Weak scaling: rank r owns global scenes [r*S, (r+1)*S) of one seeded synthetic stream
+    (pp_synth_scenes first_scene = r*S); scenes depend only on (seed, global index)."""
+    return rank * scenes_per_rank, scenes_per_rank
+
+
+def max_over_ranks(elapsed, dist, device):
+    """The job's time is the slowest rank's (MAX all-reduce; RCCL on GPUs, gloo in the CPU test)."""
+    if dist is None:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,7 +139,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     m.reserve(local, S)
-    scenes = ppamd.synth_device(m, S, seed=a.seed, first=rank * S, device=local, stream=sp)
+    first, _ = shard(rank, S)
+    scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
     res = ppamd.alloc_result(S, prm, xp="torch", device=dev)
     torch.cuda.synchronize(dev)
 
@@ -144,10 +161,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ms, launches = m.read_timing(local)
     m.timing(local, False)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, dev)
     total_cands = S * Cn * world * a.steps
     value = total_cands / elapsed
     # dominant kernel: k_cand (HIP events on the launch stream, timed region only)
