@@ -24,7 +24,9 @@ for k, d in vals.items():
     summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
 print(json.dumps(summary, indent=1))
 if tag:
-    kc = summary.get("k_cand<false>", summary.get("k_cand", {}))
+    # k_cand is launched as the fast and the slow-heading instantiation; traffic = their sum
+    parts = [v for k, v in summary.items() if k.startswith("k_cand")]
+    kc = {c: sum(p.get(c, 0.0) for p in parts) for c in set().union(*parts)} if parts else {}
     out = {}
     p = "profiles/pmc_summary.json"
     if os.path.exists(p):
@@ -34,7 +36,7 @@ if tag:
     if fetch is not None and write is not None:
         out[tag] = {"hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
                     "fetch_kib_raw": fetch, "write_kib": write,
-                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({src}); FETCH_SIZE x2 (gfx950)",
+                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), k_cand instantiations summed",
                     "counters": kc}
         json.dump(out, open(p, "w"), indent=1)
         print("wrote", p, tag)
