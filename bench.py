@@ -184,7 +184,7 @@ def main():
                    "scenes_per_gpu": S, "candidates_per_scene": Cn, "horizon_points": a.n_points,
                    "parallelism": f"scene shards x{world}, no collective"},
         "kernels_ms_avg": {"k_prep": ms[0] / max(launches[0], 1), "k_cand": k_cand_ms,
-                           "k_winner": (ms[2] / launches[2]) if launches[2] else None},
+                           "k_out": (ms[2] / launches[2]) if launches[2] else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_cand", "algorithmic_bytes_per_candidate": bpc,

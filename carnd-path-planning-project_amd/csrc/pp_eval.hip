@@ -11,7 +11,8 @@
 //                accel/curvature limiter (src/main.cpp:905-1041) reading its spline from LDS
 //                and computes the candidate cost (cost-only loop unless every path is emitted).
 //   K3 k_winner  comfort mode: per-scene argmin + re-run of the winning candidate with outputs.
-//                (reference mode: the winner is known before the loop; its k_cand lane writes them)
+//                (reference mode: the winner is known before the loop; k_cand's first wave of
+//                each block runs the winners and writes next_x/next_y)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -396,23 +397,29 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
 // ------------------------------------------------------------------------------------------------
 // Phase B: the resampling loop of one candidate (src/main.cpp:845-1041)
 // ------------------------------------------------------------------------------------------------
-struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; };
+struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj[2]; };
 
 // Output modes. The curvature adjustment (src/main.cpp:972-1018) rotates only the local->global
 // transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that the cost reads
 // never depends on it, so a cost-only lane skips the transform, its sin/cos and the stores.
-//   kOutMode 0: cost only;  2: every lane produces points;  1: lanes with out_on produce points
-//   (reference mode: the winner lane of each scene, known before the loop).
-// Point g goes to wx[g*ws], wy[g*ws] (if wx) and px[g*ps], px[g*ps+1] (if px).
+//   kOutMode 0: cost only;  2: every lane produces points;  1: lanes with out_on produce points;
+//   3: lanes with out_on RECORD their local path (pos after each step, rotation angle of each
+//   curvature adjustment + a bitmask of the adjusted steps) for k_emit, which replays the
+//   transform — the expensive sin/cos of the adjustments leaves the candidate loop entirely.
+// Point g goes to wx[g*ws], wy[g*ws] (if wx) and px[g*ps], px[g*ps+1] (if px); in mode 3 the record
+// goes to rec[g*ws] (pos_x), rec[(RN + g)*ws] (pos_y), rec[(2 RN + g)*ws] (rotation), RN = room.
 // kCache: keep the current spline segment (bounds + coefficients) in registers; the segment
 // changes every ~10-40 steps, so most steps read no slot memory.
 template <bool kLarge, int kOutMode, bool kCache>
 __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
                                  double angle, double ca0, double sa0, SC sc, int room, double* wx,
-                                 double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true) {
+                                 double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true,
+                                 double* rec = nullptr) {
     const bool kOut = kOutMode == 2 || (kOutMode == 1 && out_on);
+    const bool kRec = kOutMode == 3 && out_on;
+    const int64_t rstride = (int64_t)room * ws;
     CandRes R;
-    R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0;
+    R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0; R.adj[0] = 0; R.adj[1] = 0;
     const int nk = sl.m(0), ncp = sl.m(1), npk = sl.m(2), mflags = sl.m(3);
     if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
@@ -431,7 +438,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const double cpd = sqrt(ndx * ndx + ndy * ndy);
             if (cpd < 5) { nc++; continue; }
             cur_t += 0.02;
-            const double nca = ppm::atan2_pp(ndy, ndx);
+            const double nca = ppm::atan2_fast(ndy, ndx);
             const double adiff = ppm::fmod_2pi(nca - cang + 3 * kPi) - kPi;
             const double min_radius = s_max(10.0, speed * speed / 4);
             const double rps = speed / min_radius;
@@ -451,6 +458,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
                 if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
             }
+            if (kOutMode == 3 && kRec) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
             ng++;
             R.travelled += dstep;
         }
@@ -481,7 +489,11 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         else y = ((sa_ * h + sb) * h + sc_) * h + sy;
         const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
         double acc = fabs(speed - prev_speed) * 50;
-        const double astep = ppm::atan2_pp(y - pos_y, x - pos_x);
+#ifdef PP_ABL_NO_ATAN     // diagnostic timing build
+        const double astep = (y - pos_y) * (x - pos_x);
+#else
+        const double astep = ppm::atan2_fast(y - pos_y, x - pos_x);
+#endif
         const double adiff = ppm::fmod_2pi(astep - prev_angle + 3 * kPi) - kPi;
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
@@ -518,6 +530,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     tangle += rot;
                     ppm::sincos_pp<kLarge>(tangle, sa, ca);
                 }
+                if (kOutMode == 3 && kRec) {
+                    double nad = nc / speed / 50;
+                    if (adiff < 0) nad *= -1;
+                    rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
+                    R.adj[ng >> 6] |= 1ull << (ng & 63);
+                }
                 eff_c = nc;
                 R.flags |= PP_ST_CURV_ADJUST;
             }
@@ -535,6 +553,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
             if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
         }
+        if (kOutMode == 3 && kRec) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -592,7 +611,7 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 #endif
 template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_result out, int SPB) {
+                                              pp_result out, int SPB, double* rec, uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
     const int nslot = 3 * SPB;
@@ -619,7 +638,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         setup_lane(m, P, in, pv, s0 + j / 3, j % 3, sl);
     }
     __syncthreads();
-    const int sc_l = tid / C, c = tid - sc_l * C;
+#ifdef PP_ABL_NO_PHASE_B   // diagnostic timing build: phase A only
+    if (tid < nsc) out.status[s0 + tid] = 0;
+    return;
+#endif
+    // Lane -> candidate. Reference mode (kMode 1): lanes [0, nsc) run the scenes' winning
+    // candidates (planner lane T, max_speed: known from k_prep) and write next_x/next_y; lanes
+    // >= nsc run the C - 1 other candidates of each scene cost-only. The output work is thereby
+    // confined to the block's first wave; the other waves run the lean cost-only loop.
+    int sc_l, c;
+    if (kMode == 1) {
+        if (tid < nsc) {
+            sc_l = tid;
+            c = pv.T[s0 + tid] * NS;
+        } else {
+            const int t2 = tid - nsc;
+            sc_l = t2 / (C - 1);
+            const int r = t2 - sc_l * (C - 1);
+            const int cw = sc_l < nsc ? pv.T[s0 + sc_l] * NS : 0;
+            c = r < cw ? r : r + 1;
+        }
+    } else {
+        sc_l = tid / C;
+        c = tid - sc_l * C;
+    }
     if (sc_l < nsc && (((pv.lim_mask[s0 + sc_l] & kLimSlow) != 0) == kSlow)) {   // phase B
         const int64_t s = s0 + sc_l;
         const int L = c / NS, k = c - L * NS;
@@ -630,19 +672,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         const int K = pv.K[s], T = pv.T[s];
         // reference mode: the winning candidate (planner lane, max_speed) is known before the
         // loop, so its lane writes next_x/next_y (point-major) during the same pass
-        const bool winner = kMode != 0 && P.cost_mode == PP_COST_REFERENCE && L == T && k == 0;
-        double* wx = nullptr;
-        double* wy = nullptr;
-        if (winner) {
-            for (int i = 0; i < K; i++) {
-                out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
-                out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
-            }
-            wx = out.next_x + (int64_t)K * S + s;
-            wy = out.next_y + (int64_t)K * S + s;
-        }
+        const bool winner = kMode == 1 ? tid < nsc
+                                       : (kMode == 2 && P.cost_mode == PP_COST_REFERENCE && L == T && k == 0);
         CandRes R;
         if (kMode == 2) {
+            // every candidate writes its path; in reference mode the winner also writes next_x/y
+            double* wx = nullptr;
+            double* wy = nullptr;
+            if (winner) {
+                for (int i = 0; i < K; i++) {
+                    out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+                    out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+                }
+                wx = out.next_x + (int64_t)K * S + s;
+                wy = out.next_y + (int64_t)K * S + s;
+            }
             const int64_t ps = (int64_t)C * 2;
             double* p0 = out.paths + ((s * N) * C + c) * 2;
             for (int i = 0; i < K; i++) {
@@ -655,18 +699,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
                                                        px, ps);
             for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
             if (out.path_len) out.path_len[s * C + c] = K + R.ng;
-        } else if (kMode == 1) {
-            R = run_candidate<kSlow, 1, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
-                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K, wx, wy, S,
-                                                       nullptr, 0, winner);
+            if (winner) {
+                for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
+                out.n_out[s] = K + R.ng;
+                out.winner[s] = c;
+            }
+        } else if (kMode == 1 && tid < 64) {
+            // reference mode, the block's first wave: the winners record their local path
+            // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
+            R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
+                                                       S, nullptr, 0, winner, rec + s);
+            if (winner) {
+                out.n_out[s] = K + R.ng;
+                out.winner[s] = c;
+                adjm[s] = R.adj[0];
+                adjm[S + s] = R.adj[1];
+            }
         } else {
             R = run_candidate<kSlow, 0, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
                                                        nullptr, nullptr, 0, nullptr, 0);
-        }
-        if (winner) {
-            for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
-            out.n_out[s] = K + R.ng;
-            out.winner[s] = c;
         }
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
@@ -680,17 +731,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3 (comfort mode): per-scene argmin over the candidate costs (first minimum, as the oracle), then
-// the winning candidate re-run with outputs. One lane per scene; next_x/next_y are point-major
-// ([i * S + s], the batch's own convention), so every step of a wave stores 512 contiguous bytes.
+// K3: per-scene winner: argmin over the candidate costs (first minimum, as the oracle; in
+// reference mode that is the planner's candidate), then the winning candidate re-run with outputs.
+// One lane per scene, 64 scenes per block; each lane's spline slot lives in LDS (kWinKnots =
+// 9 previous + 6 control points, the real maximum) so 4 blocks fit a CU; with the segment cache
+// the loop rarely reads it. next_x/next_y are point-major ([i * S + s], the batch's own
+// convention): every step of the wave stores 512 contiguous bytes.
 // ------------------------------------------------------------------------------------------------
-constexpr int kWinBlock = 256;
+constexpr int kWinBlock = 64;
+constexpr int kWinKnots = 15;
+static_assert(PP_PREV_KEEP - 1 + 6 <= kWinKnots, "slot too small");
 template <bool kSlow>
 __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in, pp_params P,
-                                                      PrepV pv, pp_result out, double* spl) {
+                                                      PrepV pv, pp_result out) {
+    __shared__ __attribute__((aligned(16))) double wsm[5 * kWinKnots * kWinBlock];
+    __shared__ int wmeta[4 * kWinBlock];
     const MapV m = map_view(mg.buf, mg.n);
     const int64_t S = in.n_scenes;
-    const int64_t s = (int64_t)blockIdx.x * kWinBlock + threadIdx.x;
+    const int j = threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * kWinBlock + j;
     if (s >= S || ((pv.lim_mask[s] & kLimSlow) != 0) != kSlow) return;
     const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
     int best = 0;
@@ -700,10 +759,10 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         if (v < bc) { bc = v; best = c; }
     }
     const int L = best / NS, k = best - L * NS;
-    // strided scratch [field][knot][S]: a wave's accesses to one knot are 512 contiguous bytes
-    const int64_t KS = (int64_t)PP_MAX_KNOTS * S;
-    const Slot sl = {spl + s, spl + KS + s, spl + 2 * KS + s, spl + 3 * KS + s, spl + 4 * KS + s,
-                     (int*)(spl + 5 * KS) + s, S};
+    // slot arrays interleaved by lane ([knot][lane]) so the 64 lanes' accesses spread over banks
+    const Slot sl = {wsm + j, wsm + kWinKnots * kWinBlock + j, wsm + 2 * kWinKnots * kWinBlock + j,
+                     wsm + 3 * kWinKnots * kWinBlock + j, wsm + 4 * kWinKnots * kWinBlock + j,
+                     wmeta + j, kWinBlock};
     setup_lane(m, P, in, pv, s, L, sl);
     const double v = cand_speed(P, pv.ego_speed[s], k);
     const SC sc = make_sc(P, pv, S, s, L, v);
@@ -719,6 +778,60 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
     out.n_out[s] = K + R.ng;
     out.winner[s] = best;
+}
+
+// ------------------------------------------------------------------------------------------------
+// K4 (reference mode): next_x/next_y of the winner from its recorded local path — the output
+// transform of TrajectoryBuilder::build replayed exactly: at each recorded curvature adjustment
+// the transform centre is rotated about the current point and the frame angle advanced
+// (src/main.cpp:994-1007), every point is mapped back with the current frame (:1033-1037). One lane
+// per scene; all loads/stores point-major (coalesced).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+                                              const double* rec, const uint64_t* adjm) {
+    const int64_t S = in.n_scenes;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int N = P.n_points;
+    const int K = pv.K[s];
+    const int room = N - K;
+    const int ng = out.n_out[s] - K;
+    const int64_t rstride = (int64_t)room * S;
+    for (int i = 0; i < K; i++) {
+        out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+        out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+    }
+    double cx = pv.pos_x[s], cy = pv.pos_y[s], tangle = pv.angle[s];
+    double ca = pv.ca_p[s], sa = pv.sa_p[s];
+    const uint64_t m0 = adjm[s], m1 = adjm[S + s];
+    double pxp = 0, pyp = 0;                       // local position before the step
+    for (int g = 0; g < ng; g++) {
+        const uint64_t bit = g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1;
+        if (bit) {
+            const double rot = rec[2 * rstride + (int64_t)g * S + s];
+            double tpx = pxp * ca - pyp * sa;
+            double tpy = pxp * sa + pyp * ca;
+            tpx = tpx + cx;
+            tpy = tpy + cy;
+            const double vx = cx - tpx, vy = cy - tpy;
+            double cr, sr;
+            ppm::sincos_pp<true>(rot, sr, cr);
+            const double rvx = vx * cr - vy * sr;
+            const double rvy = vx * sr + vy * cr;
+            cx = tpx + rvx;
+            cy = tpy + rvy;
+            tangle += rot;
+            ppm::sincos_pp<true>(tangle, sa, ca);
+        }
+        const double px_ = rec[(int64_t)g * S + s], py_ = rec[rstride + (int64_t)g * S + s];
+        const double tx = px_ * ca - py_ * sa;
+        const double ty = px_ * sa + py_ * ca;
+        out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
+        out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+        pxp = px_;
+        pyp = py_;
+    }
+    for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -850,9 +963,11 @@ int dev_init(pp_map* M, int device) {
 }
 
 size_t prep_bytes(int64_t S) { return ((size_t)S * (kPrepD * 8 + kPrepI * 4) + 255) / 256 * 256; }
-// k_winner scratch: 5 double arrays [PP_MAX_KNOTS][S] + 4 int arrays [S]
-size_t spline_bytes(int64_t S) { return (size_t)S * (5 * PP_MAX_KNOTS * 8 + 4 * 4) + 256; }
-double* spline_scratch(void* ws, int64_t cap) { return (double*)((char*)ws + prep_bytes(cap)); }
+// reference-mode winner record (k_cand -> k_emit): 3 x PP_MAX_POINTS x S doubles + 2 x S u64
+size_t rec_bytes(int64_t S) { return (size_t)S * (3 * PP_MAX_POINTS + 2) * 8 + 256; }
+double* rec_buf(void* ws, int64_t cap) { return (double*)((char*)ws + prep_bytes(cap)); }
+uint64_t* adj_buf(void* ws, int64_t cap) { return (uint64_t*)(rec_buf(ws, cap) + 3 * PP_MAX_POINTS * cap); }
+
 
 PrepV prep_bind(void* base, int64_t S) {
     PrepV p;
@@ -877,7 +992,7 @@ int ensure_ws(pp_map* M, int device, int64_t S) {
     DevState& D = M->dev[device];
     if (D.ws_cap >= S) return PP_OK;
     if (D.ws) { (void)hipDeviceSynchronize(); (void)hipFree(D.ws); D.ws = nullptr; D.ws_cap = 0; }
-    if (hipMalloc(&D.ws, prep_bytes(S) + spline_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMalloc(&D.ws, prep_bytes(S) + rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
     D.ws_cap = S;
     return PP_OK;
 }
@@ -981,7 +1096,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const int64_t S = in->n_scenes;
     PrepV pv;
     MapG mg;
-    double* spl = nullptr;
+    double* rec = nullptr;
+    uint64_t* adjm = nullptr;
     {
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
@@ -989,7 +1105,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         rc = ensure_ws(M, device, S);
         if (rc) return rc;
         pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
-        spl = spline_scratch(M->dev[device].ws, M->dev[device].ws_cap);
+        rec = rec_buf(M->dev[device].ws, M->dev[device].ws_cap);
+        adjm = adj_buf(M->dev[device].ws, M->dev[device].ws_cap);
         mg.buf = M->dev[device].map;
         mg.n = M->n;
     }
@@ -1010,7 +1127,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 D.ev_pool.pop_back();
                 D.ev_rec.push_back(ev[i]);
             }
-            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT ? 1 : 0);
+            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT || !prm->emit_paths ? 1 : 0);
         }
     }
     pp_params P = *prm;
@@ -1035,22 +1152,27 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const int64_t blocks = (S + spb - 1) / spb;
         if (timing) (void)hipEventRecord(ev[1], st);
         if (P.emit_paths) {
-            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
         } else if (P.cost_mode == PP_COST_REFERENCE) {
-            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
         } else {
-            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
-            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb);
+            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
         }
     }
     if (timing) (void)hipEventRecord(ev[2], st);
-    // K3 (comfort mode): argmin + winner path; scratch regions are sized to ws_cap >= S
+    // K4 (reference mode, winner-only output): replay the winners' recorded paths
+    if (P.cost_mode == PP_COST_REFERENCE && !P.emit_paths) {
+        const int64_t blocks = (S + 255) / 256;
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm);
+    }
+    // K3 (comfort mode): argmin + winner path (reference mode: k_cand's winner lanes wrote it)
     if (P.cost_mode == PP_COST_COMFORT) {
         const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
-        hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);
-        hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R, spl);
+        hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+        hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
     }
     if (timing) (void)hipEventRecord(ev[3], st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;

@@ -193,6 +193,52 @@ __device__ __forceinline__ double atan2_pp(double y, double x) {
     }
 }
 
+// Branch-free atan2 for finite nonzero (y, x): ONE division and no divergent interval branches.
+// The argument reduction of atan_pos is applied to (|y|, |x|) directly — e.g. t = (|y|-|x|) /
+// (|x|+|y|) instead of (q-1)/(q+1) with a rounded q = |y|/|x| — so the reduced argument carries a
+// single rounding (slightly more accurate than the two-division form). Interval selection by
+// exact comparisons of |y| against 7/16, 11/16, 19/16, 39/16 times |x| (scaled by 16, exact in
+// double for the magnitudes that reach this path); the quadrant logic is atan2_pp's.
+__device__ __forceinline__ double atan2_fast(double y, double x) {
+    const double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    const int hx = hiword(x), hy = hiword(y);
+    const int ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    const bool x_special = (ix | loword(x)) == 0 || ix >= 0x7ff00000;
+    const bool y_special = (iy | loword(y)) == 0 || iy >= 0x7ff00000;
+    const int k = (iy - ix) >> 20;
+    if (__builtin_expect(x_special || y_special || k > 60 || k < -60, 0)) return atan2_pp(y, x);
+    const double ay = fabs(y), ax = fabs(x);
+    const double y16 = 16.0 * ay;
+    // interval id: -1 (q < 7/16), 0 (< 11/16), 1 (< 19/16), 2 (< 39/16), 3 (>= 39/16)
+    const int id = (y16 < 7.0 * ax) ? -1 : (y16 < 11.0 * ax) ? 0 : (y16 < 19.0 * ax) ? 1
+                 : (y16 < 39.0 * ax) ? 2 : 3;
+    // t = num / den per interval (fdlibm's reductions multiplied through by |x|)
+    double num, den, hi, lo;
+    if (id < 0)       { num = ay;                  den = ax;                  hi = 0.0; lo = 0.0; }
+    else if (id == 0) { num = 2.0 * ay - ax;       den = 2.0 * ax + ay;
+                        hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+    else if (id == 1) { num = ay - ax;             den = ax + ay;
+                        hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+    else if (id == 2) { num = 2.0 * ay - 3.0 * ax; den = 2.0 * ax + 3.0 * ay;
+                        hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+    else              { num = -ax;                 den = ay;
+                        hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    const double t = num / den;
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const double z = t * t;
+    const double w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const double zz = (id < 0) ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);  // 2*sign(x) + sign(y)
+    return m == 0 ? zz : m == 1 ? -zz : m == 2 ? pi - (zz - pi_lo) : (zz - pi_lo) - pi;
+}
+
 // fmod(a, 2*pi) for the reference's angle wrap fmod(d + 3*pi, 2*pi) - pi
 // (src/main.cpp:870, 934). fmod is exact, so any exact evaluation is bit-identical: for
 // 0 <= a < 3*(2*pi) the remainder a - k*(2*pi), k in {0, 1, 2}, is computed exactly
