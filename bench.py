@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--n-points", type=int, default=50)
     ap.add_argument("--emit-paths", action="store_true", help="write every candidate path (config 3)")
     ap.add_argument("--comfort", action="store_true", help="comfort cost mode (data-dependent argmin)")
+    ap.add_argument("--draws", type=int, default=0,
+                    help="Monte-Carlo sensor-noise draws per scene (config 4: --scenes 16384 --draws 64 --n-speeds 1)")
     ap.add_argument("--seed", type=int, default=0x5EED0001)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -72,7 +74,7 @@ def cpu_baseline(m, scenes_dev, prm, budget_s):
     import oracle_lib
     import ppamd
     wx, wy = ppamd.highway_map()
-    rlib = oracle_lib.load_ref() if prm.n_points == 50 and not prm.emit_paths else None
+    rlib = oracle_lib.load_ref() if prm.n_points == 50 and not prm.emit_paths and prm.n_draws <= 1 else None
     olib = None if rlib else oracle_lib.load_oracle()
     chunk = 2048
     S = int(scenes_dev["ego_x"].shape[0])
@@ -88,10 +90,10 @@ def cpu_baseline(m, scenes_dev, prm, budget_s):
         t_used += time.perf_counter() - t0
         done += host["ego_x"].shape[0]
         start += chunk
-    cands = done * 3 * prm.n_speeds
+    cands = done * 3 * prm.n_speeds * max(prm.n_draws, 1)
     return {"value": cands / t_used, "unit": "candidate trajectories/s", "cores": 1,
             "kind": "reference" if rlib else "port",
-            "sample": f"first {done} scenes x {3 * prm.n_speeds} candidates of the same synthetic "
+            "sample": f"first {done} scenes x {3 * prm.n_speeds * max(prm.n_draws, 1)} candidates of the same synthetic "
                       f"batch ({t_used:.1f} s, single thread; "
                       + ("reference src/main.cpp classes built by oracle/Makefile" if rlib else
                          "C restatement oracle/pp_oracle.c") + ")"}
@@ -133,13 +135,15 @@ def main():
     S = a.scenes
     prm = ppamd.default_params(n_speeds=a.n_speeds, n_points=a.n_points,
                                cost_mode=ppamd.COST_COMFORT if a.comfort else ppamd.COST_REFERENCE,
-                               emit_paths=a.emit_paths,
+                               emit_paths=a.emit_paths, n_draws=a.draws, noise_first_scene=0,
                                speed_offsets=[-6, -4, -3, -2, -1, 0, 2] if a.n_speeds == 8 else None)
-    Cn = 3 * a.n_speeds
+    D = max(a.draws, 1)
+    Cn = D * 3 * a.n_speeds
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-    m.reserve(local, S)
+    m.reserve(local, S * D)
     first, _ = shard(rank, S)
+    prm.noise_first_scene = first
     scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
     res = ppamd.alloc_result(S, prm, xp="torch", device=dev)
     torch.cuda.synchronize(dev)
@@ -169,7 +173,7 @@ def main():
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
     bytes_launch = bpc * S * Cn
     achieved = bytes_launch / (k_cand_ms * 1e-3) / 1e9
-    tag = f"k_cand_S{S}_C{Cn}_N{a.n_points}" + ("_paths" if a.emit_paths else "")
+    tag = f"k_cand_S{S}_C{Cn}_N{a.n_points}" + ("_paths" if a.emit_paths else "") + (f"_D{D}" if D > 1 else "")
     traffic, traffic_src = load_traffic(tag)
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",
@@ -177,8 +181,10 @@ def main():
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (Philox scenes on highway_map.csv, seeded; SURVEY.md §8(d))",
-        "config": {"workload": f"BASELINE config 5 batch: {S} scenes x 3 lanes x {a.n_speeds} speeds, "
-                               f"{a.n_points}-pt horizon per GPU"
+        "config": {"workload": (f"BASELINE config 4: {S} scenes x {D} sensor-noise draws x 3 lanes x "
+                                f"{a.n_speeds} speeds, per-scene argmin over draws" if D > 1 else
+                                f"BASELINE config 5 batch: {S} scenes x 3 lanes x {a.n_speeds} speeds")
+                               + f", {a.n_points}-pt horizon per GPU"
                                + (", all paths emitted" if a.emit_paths else ", winner path + costs")
                                + (", comfort cost" if a.comfort else ", reference decision"),
                    "scenes_per_gpu": S, "candidates_per_scene": Cn, "horizon_points": a.n_points,

@@ -49,15 +49,21 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 }
 
 __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_scene_info* info) {
+                                              pp_scene_info* info, uint32_t* out_status) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
     for (int i = threadIdx.x; i < 13 * n; i += blockDim.x) smap[i] = mg.buf[i];
     __syncthreads();
     const MapV m = map_view(smap, n);
+    // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
+    // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= Sv) return;
+    const int64_t s = D == 1 ? v : v / D;
+    const int draw = (int)(v - s * D);
 
     uint32_t status = 0;
     // ---- ego derivation (src/main.cpp:1233-1292) ----
@@ -115,7 +121,14 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
     for (int j = 0; j < ncar; j++) {
         const int64_t ix = (int64_t)j * S + s;
         const int id = in.car_id[ix];
-        const double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+        double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+        if (draw > 0) {                     // Monte-Carlo sensor noise (include/pp.h pp_params)
+            const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+            cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 0);
+            cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 1);
+            cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 2);
+            cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 3);
+        }
         double cs, cd;
         int clane = 0, nwp = 0;
         if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
@@ -208,7 +221,7 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
         double ts, tt;
         const int code = limit_speed(P, in_vx, in_vy, in_s, ego_s, ego_speed, ego_acc, true, ts, tt, col);
         status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
-        pv.in_ts[s] = ts; pv.in_tt[s] = tt;
+        pv.in_ts[v] = ts; pv.in_tt[v] = tt;
         lim_mask |= 1;
     }
 #pragma unroll
@@ -217,7 +230,7 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
             double ts, tt;
             const int code = limit_speed(P, t_vx[L], t_vy[L], t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
             status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
-            pv.l_ts[L * S + s] = ts; pv.l_tt[L * S + s] = tt;
+            pv.l_ts[L * Sv + v] = ts; pv.l_tt[L * Sv + v] = tt;
             lim_mask |= 2 << L;
         }
     }
@@ -235,18 +248,19 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
     // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
     // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
     if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
-    pv.pos_x[s] = pos_x; pv.pos_y[s] = pos_y; pv.angle[s] = angle;
+    pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
     double cm, sm, cp, sp_;
     ppm::sincos_pp<true>(-angle, sm, cm);
     ppm::sincos_pp<true>(angle, sp_, cp);
-    pv.ca_m[s] = cm; pv.sa_m[s] = sm;
-    pv.ca_p[s] = cp; pv.sa_p[s] = sp_;
-    pv.ego_speed[s] = ego_speed; pv.ego_d[s] = ego_d; pv.ego_vd[s] = ego_vd;
+    pv.ca_m[v] = cm; pv.sa_m[v] = sm;
+    pv.ca_p[v] = cp; pv.sa_p[v] = sp_;
+    pv.ego_speed[v] = ego_speed; pv.ego_d[v] = ego_d; pv.ego_vd[v] = ego_vd;
 #pragma unroll
-    for (int l = 0; l < 3; l++) { pv.ratio[l * S + s] = ratio[l]; pv.score[l * S + s] = score[l]; }
-    pv.K[s] = K; pv.ref_wp[s] = ref_wp; pv.T[s] = T; pv.ego_lane[s] = ego_lane;
-    pv.open_mask[s] = open_mask; pv.lim_mask[s] = lim_mask; pv.status[s] = status;
-    if (info) {
+    for (int l = 0; l < 3; l++) { pv.ratio[l * Sv + v] = ratio[l]; pv.score[l * Sv + v] = score[l]; }
+    pv.K[v] = K; pv.ref_wp[v] = ref_wp; pv.T[v] = T; pv.ego_lane[v] = ego_lane;
+    pv.open_mask[v] = open_mask; pv.lim_mask[v] = lim_mask; pv.status[v] = status;
+    if (draw == 0) out_status[s] = 0;        // k_cand ORs its flags in (atomics when a scene spans blocks)
+    if (info && draw == 0) {
         pp_scene_info I = {};
         I.ego_x = ego_x; I.ego_y = ego_y; I.ego_speed = ego_speed; I.ego_acc = ego_acc;
         I.ego_s = ego_s; I.ego_d = ego_d; I.ego_vs = ego_vs; I.ego_vd = ego_vd;
@@ -276,15 +290,17 @@ struct Slot {
 };
 constexpr int kMetaFallback = 1, kMetaTrunc = 2, kMetaWalkFail = 4;
 
+// s: scene (inputs, stride in.n_scenes); v: its prep record (stride Sv). The spline depends on the
+// ego state only (no sensor-fusion input), so every Monte-Carlo draw of a scene shares it.
 __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_batch& in,
-                           const PrepV& pv, int64_t s, int L, const Slot& sl) {
+                           const PrepV& pv, int64_t s, int64_t v, int64_t Sv, int L, const Slot& sl) {
     const int64_t S = in.n_scenes;
-    const int K = pv.K[s];
-    const double pos_x = pv.pos_x[s], pos_y = pv.pos_y[s];
-    const double ca = pv.ca_m[s], sa = pv.sa_m[s];
-    const double start = pv.ego_speed[s], ego_d = pv.ego_d[s], ego_vd = pv.ego_vd[s];
-    const int ref_wp = pv.ref_wp[s];
-    const double ratio = pv.ratio[L * S + s];
+    const int K = pv.K[v];
+    const double pos_x = pv.pos_x[v], pos_y = pv.pos_y[v];
+    const double ca = pv.ca_m[v], sa = pv.sa_m[v];
+    const double start = pv.ego_speed[v], ego_d = pv.ego_d[v], ego_vd = pv.ego_vd[v];
+    const int ref_wp = pv.ref_wp[v];
+    const double ratio = pv.ratio[L * Sv + v];
     int flags = 0;
     // lane switch time / first control point distance (src/main.cpp:640-731)
     double min_cpd = start * 1;
@@ -611,9 +627,11 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 #endif
 template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_result out, int SPB, double* rec, uint64_t* adjm) {
+                                              pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
+    const int NS = P.n_speeds, Cv = 3 * NS, N = P.n_points;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int C = D * Cv;                     // candidates per scene (all draws)
     const int nslot = 3 * SPB;
     double* sX = sm;
     double* sY = sX + nslot * kKP;
@@ -624,28 +642,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
     uint32_t* sFlags = (uint32_t*)(sMeta + 4 * nslot);
     const MapV m = map_view(mg.buf, mg.n);
     const int64_t S = in.n_scenes;
-    const int64_t s0 = (int64_t)blockIdx.x * SPB;
+    const int64_t Sv = S * D;
+    // block -> scenes: BPS == 1: SPB whole scenes; BPS > 1 (C > 256): one scene, candidates
+    // [coff, coff + 256) of it
+    int64_t s0;
+    int coff;
+    if (BPS == 1) { s0 = (int64_t)blockIdx.x * SPB; coff = 0; }
+    else { s0 = blockIdx.x / BPS; coff = (int)(blockIdx.x - s0 * BPS) * 256; }
     const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
     const int tid = threadIdx.x;
     if (kSlow) {   // whole block leaves unless one of its scenes is flagged
-        const bool mine = tid < nsc && (pv.lim_mask[s0 + tid] & kLimSlow);
+        const bool mine = tid < nsc && (pv.lim_mask[(s0 + tid) * D] & kLimSlow);
         if (!__syncthreads_or(mine)) return;
     }
     if (tid < SPB) sFlags[tid] = 0;
-    if (tid < 3 * nsc && (((pv.lim_mask[s0 + tid / 3] & kLimSlow) != 0) == kSlow)) {   // phase A
+    if (tid < 3 * nsc && (((pv.lim_mask[(s0 + tid / 3) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
         const int j = tid;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
-        setup_lane(m, P, in, pv, s0 + j / 3, j % 3, sl);
+        setup_lane(m, P, in, pv, s0 + j / 3, (s0 + j / 3) * D, Sv, j % 3, sl);
     }
     __syncthreads();
 #ifdef PP_ABL_NO_PHASE_B   // diagnostic timing build: phase A only
     if (tid < nsc) out.status[s0 + tid] = 0;
     return;
 #endif
-    // Lane -> candidate. Reference mode (kMode 1): lanes [0, nsc) run the scenes' winning
-    // candidates (planner lane T, max_speed: known from k_prep) and write next_x/next_y; lanes
-    // >= nsc run the C - 1 other candidates of each scene cost-only. The output work is thereby
-    // confined to the block's first wave; the other waves run the lean cost-only loop.
+    // Lane -> candidate. Reference mode without draws (kMode 1): lanes [0, nsc) run the scenes'
+    // winning candidates (planner lane T, max_speed: known from k_prep) and record their paths;
+    // lanes >= nsc run the C - 1 other candidates of each scene cost-only. The output work is
+    // thereby confined to the block's first wave; the other waves run the lean cost-only loop.
     int sc_l, c;
     if (kMode == 1) {
         if (tid < nsc) {
@@ -659,17 +683,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
             c = r < cw ? r : r + 1;
         }
     } else {
-        sc_l = tid / C;
-        c = tid - sc_l * C;
+        const int t = tid + coff;
+        sc_l = t / C;
+        c = t - sc_l * C;
     }
-    if (sc_l < nsc && (((pv.lim_mask[s0 + sc_l] & kLimSlow) != 0) == kSlow)) {   // phase B
+    if (sc_l < nsc && c < C && (((pv.lim_mask[(s0 + sc_l) * D] & kLimSlow) != 0) == kSlow)) {   // phase B
         const int64_t s = s0 + sc_l;
-        const int L = c / NS, k = c - L * NS;
+        const int d = c / Cv, cc = c - d * Cv;
+        const int64_t v = s * D + d;              // this draw's prep record
+        const int L = cc / NS, k = cc - L * NS;
         const int j = sc_l * 3 + L;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
-        const double v = cand_speed(P, pv.ego_speed[s], k);
-        const SC sc = make_sc(P, pv, S, s, L, v);
-        const int K = pv.K[s], T = pv.T[s];
+        const double vt = cand_speed(P, pv.ego_speed[v], k);
+        const SC sc = make_sc(P, pv, Sv, v, L, vt);
+        const int K = pv.K[v], T = pv.T[v];
         // reference mode: the winning candidate (planner lane, max_speed) is known before the
         // loop, so its lane writes next_x/next_y (point-major) during the same pass
         const bool winner = kMode == 1 ? tid < nsc
@@ -694,8 +721,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
                 p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
             }
             double* px = p0 + K * ps;
-            R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
-                                                       pv.ca_p[s], pv.sa_p[s], sc, N - K, wx, wy, S,
+            R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
+                                                       pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
                                                        px, ps);
             for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
             if (out.path_len) out.path_len[s * C + c] = K + R.ng;
@@ -720,19 +747,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
                                                        nullptr, nullptr, 0, nullptr, 0);
         }
         uint32_t flags = R.flags;
-        const double cost = cand_cost(P, R, K, pv.score[L * S + s], L, T, v, pv.open_mask[s],
-                                      pv.ego_lane[s], flags);
+        const double cost = cand_cost(P, R, K, pv.score[L * Sv + v], L, T, vt, pv.open_mask[v],
+                                      pv.ego_lane[v], flags);
         out.cost[s * C + c] = cost;
+        if (D > 1) flags |= (uint32_t)pv.status[v];     // every draw's planner flags
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
-    if (tid < nsc && (((pv.lim_mask[s0 + tid] & kLimSlow) != 0) == kSlow))
-        out.status[s0 + tid] = (uint32_t)pv.status[s0 + tid] | sFlags[tid];
+    if (tid < nsc && (((pv.lim_mask[(s0 + tid) * D] & kLimSlow) != 0) == kSlow)) {
+        const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
+        if (BPS == 1) out.status[s0 + tid] = st;
+        else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
-// K3: per-scene winner: argmin over the candidate costs (first minimum, as the oracle; in
-// reference mode that is the planner's candidate), then the winning candidate re-run with outputs.
+// K3: per-scene winner: argmin over the candidate costs (first minimum, as the oracle; with
+// Monte-Carlo draws over the draw-averaged cost of each (lane, speed)), then the winning
+// candidate re-run on the nominal scene with outputs.
 // One lane per scene, 64 scenes per block; each lane's spline slot lives in LDS (kWinKnots =
 // 9 previous + 6 control points, the real maximum) so 4 blocks fit a CU; with the segment cache
 // the loop rarely reads it. next_x/next_y are point-major ([i * S + s], the batch's own
@@ -748,31 +780,39 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     __shared__ int wmeta[4 * kWinBlock];
     const MapV m = map_view(mg.buf, mg.n);
     const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
     const int j = threadIdx.x;
     const int64_t s = (int64_t)blockIdx.x * kWinBlock + j;
-    if (s >= S || ((pv.lim_mask[s] & kLimSlow) != 0) != kSlow) return;
-    const int NS = P.n_speeds, C = 3 * NS, N = P.n_points;
+    const int64_t v0 = s * D;                 // the nominal (draw 0) prep record
+    if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
+    const int NS = P.n_speeds, Cv = 3 * NS, C = D * Cv, N = P.n_points;
+    // decision: first minimum over (lane, k) of the cost averaged over the draws (summed in draw
+    // order, then / D; D = 1: the plain cost)
     int best = 0;
-    double bc = out.cost[s * C];
-    for (int c = 1; c < C; c++) {
-        const double v = out.cost[s * C + c];
-        if (v < bc) { bc = v; best = c; }
+    double bc = 0;
+    for (int c = 0; c < Cv; c++) {
+        double sum = out.cost[s * C + c];
+        for (int d = 1; d < D; d++) sum += out.cost[s * C + d * Cv + c];
+        const double mean = sum / D;
+        if (out.draw_mean_cost) out.draw_mean_cost[s * Cv + c] = mean;
+        if (c == 0 || mean < bc) { bc = mean; best = c; }
     }
     const int L = best / NS, k = best - L * NS;
     // slot arrays interleaved by lane ([knot][lane]) so the 64 lanes' accesses spread over banks
     const Slot sl = {wsm + j, wsm + kWinKnots * kWinBlock + j, wsm + 2 * kWinKnots * kWinBlock + j,
                      wsm + 3 * kWinKnots * kWinBlock + j, wsm + 4 * kWinKnots * kWinBlock + j,
                      wmeta + j, kWinBlock};
-    setup_lane(m, P, in, pv, s, L, sl);
-    const double v = cand_speed(P, pv.ego_speed[s], k);
-    const SC sc = make_sc(P, pv, S, s, L, v);
-    const int K = pv.K[s];
+    setup_lane(m, P, in, pv, s, v0, Sv, L, sl);
+    const double v = cand_speed(P, pv.ego_speed[v0], k);
+    const SC sc = make_sc(P, pv, Sv, v0, L, v);
+    const int K = pv.K[v0];
     for (int i = 0; i < K; i++) {
         out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
         out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
     }
-    const CandRes R = run_candidate<kSlow, 2, true>(P, sl, pv.pos_x[s], pv.pos_y[s], pv.angle[s],
-                                                    pv.ca_p[s], pv.sa_p[s], sc, N - K,
+    const CandRes R = run_candidate<kSlow, 2, true>(P, sl, pv.pos_x[v0], pv.pos_y[v0], pv.angle[v0],
+                                                    pv.ca_p[v0], pv.sa_p[v0], sc, N - K,
                                                     out.next_x + (int64_t)K * S + s,
                                                     out.next_y + (int64_t)K * S + s, S, nullptr, 0);
     for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
@@ -857,8 +897,10 @@ struct DevState {
     bool init = false;
     double* map = nullptr;        // 13 * n
     double* lanetab = nullptr;    // synth tables: lc_x[3n] lc_y[3n] seg_len[3n] tan_x[3n] tan_y[3n]
-    void* ws = nullptr;           // prep workspace
+    void* ws = nullptr;           // prep workspace (per evaluation: scene x draw)
     int64_t ws_cap = 0;
+    void* rec = nullptr;          // reference-mode winner record (per scene)
+    int64_t rec_cap = 0;
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
     bool timing = false;          // pp_timing_enable
     std::vector<hipEvent_t> ev_pool;
@@ -965,8 +1007,8 @@ int dev_init(pp_map* M, int device) {
 size_t prep_bytes(int64_t S) { return ((size_t)S * (kPrepD * 8 + kPrepI * 4) + 255) / 256 * 256; }
 // reference-mode winner record (k_cand -> k_emit): 3 x PP_MAX_POINTS x S doubles + 2 x S u64
 size_t rec_bytes(int64_t S) { return (size_t)S * (3 * PP_MAX_POINTS + 2) * 8 + 256; }
-double* rec_buf(void* ws, int64_t cap) { return (double*)((char*)ws + prep_bytes(cap)); }
-uint64_t* adj_buf(void* ws, int64_t cap) { return (uint64_t*)(rec_buf(ws, cap) + 3 * PP_MAX_POINTS * cap); }
+double* rec_buf(void* rec) { return (double*)rec; }
+uint64_t* adj_buf(void* rec, int64_t cap) { return (uint64_t*)((double*)rec + 3 * PP_MAX_POINTS * cap); }
 
 
 PrepV prep_bind(void* base, int64_t S) {
@@ -988,14 +1030,25 @@ PrepV prep_bind(void* base, int64_t S) {
     return p;
 }
 
-int ensure_ws(pp_map* M, int device, int64_t S) {
+int ensure_ws(pp_map* M, int device, int64_t Sv) {
     DevState& D = M->dev[device];
-    if (D.ws_cap >= S) return PP_OK;
+    if (D.ws_cap >= Sv) return PP_OK;
     if (D.ws) { (void)hipDeviceSynchronize(); (void)hipFree(D.ws); D.ws = nullptr; D.ws_cap = 0; }
-    if (hipMalloc(&D.ws, prep_bytes(S) + rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
-    D.ws_cap = S;
+    if (hipMalloc(&D.ws, prep_bytes(Sv)) != hipSuccess) return PP_ERR_NOMEM;
+    D.ws_cap = Sv;
     return PP_OK;
 }
+
+int ensure_rec(pp_map* M, int device, int64_t S) {
+    DevState& D = M->dev[device];
+    if (D.rec_cap >= S) return PP_OK;
+    if (D.rec) { (void)hipDeviceSynchronize(); (void)hipFree(D.rec); D.rec = nullptr; D.rec_cap = 0; }
+    if (hipMalloc(&D.rec, rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
+    D.rec_cap = S;
+    return PP_OK;
+}
+
+int n_draws(const pp_params* p) { return p->n_draws > 1 ? p->n_draws : 1; }
 
 int cands_per_block(int C) {
     int spb = 256 / C;
@@ -1007,7 +1060,9 @@ int cands_per_block(int C) {
 bool params_ok(const pp_params* p) {
     return p && p->n_points > PP_PREV_KEEP && p->n_points <= PP_MAX_POINTS && p->n_speeds >= 1 &&
            p->n_speeds <= PP_MAX_SPEEDS && 3 * p->n_speeds <= 256 &&
-           (p->cost_mode == PP_COST_REFERENCE || p->cost_mode == PP_COST_COMFORT);
+           (p->cost_mode == PP_COST_REFERENCE || p->cost_mode == PP_COST_COMFORT) &&
+           p->n_draws >= 0 && p->n_draws <= PP_MAX_DRAWS && p->noise_first_scene >= 0 &&
+           !(p->n_draws > 1 && p->emit_paths);
 }
 
 }  // namespace
@@ -1031,9 +1086,18 @@ void pp_params_default(pp_params* p) {
     p->safety_distance = 2;
     p->keep_distance = 10;
     p->keep_distance_leeway = 0.5;
+    p->n_draws = 0;
+    p->noise_seed = 0x5EED0002ull;
+    p->noise_first_scene = 0;
+    p->noise_pos_sigma = 0.5;            // SURVEY.md §8(d) Monte-Carlo
+    p->noise_vel_sigma = 0.5;
 }
 
-int32_t pp_num_candidates(const pp_params* p) { return p ? 3 * p->n_speeds : 0; }
+int32_t pp_num_candidates(const pp_params* p) { return p ? n_draws(p) * 3 * p->n_speeds : 0; }
+
+double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q) {
+    return ppsynth::mc_gauss(seed, (uint64_t)scene, draw, car, q);
+}
 
 const char* pp_version(void) { return "pp-mi355x 0.1 (gfx950, fp64, lane-per-candidate)"; }
 
@@ -1056,6 +1120,7 @@ int32_t pp_map_destroy(pp_map* M) {
         (void)hipDeviceSynchronize();
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
         if (D.ws) (void)hipFree(D.ws);
+        if (D.rec) (void)hipFree(D.rec);
         if (D.frame) (void)hipFree(D.frame);
         for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : D.ev_rec) (void)hipEventDestroy(e);
@@ -1076,7 +1141,9 @@ int32_t pp_reserve(pp_map* M, int32_t device, int64_t max_scenes) {
     DeviceGuard g(device);
     int rc = dev_init(M, device);
     if (rc) return rc;
-    return ensure_ws(M, device, max_scenes);
+    rc = ensure_ws(M, device, max_scenes);
+    if (rc) return rc;
+    return ensure_rec(M, device, max_scenes);
 }
 
 int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
@@ -1094,6 +1161,11 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)hip_stream;
     const int64_t S = in->n_scenes;
+    const int Dn = n_draws(prm);
+    const int64_t Sv = S * Dn;                    // evaluations (scene x draw)
+    // reference decision without draws: the winner is known before the loop (k_cand records it,
+    // k_emit writes it); otherwise the decision is a cost argmin (k_winner)
+    const bool ref_direct = prm->cost_mode == PP_COST_REFERENCE && Dn == 1;
     PrepV pv;
     MapG mg;
     double* rec = nullptr;
@@ -1102,11 +1174,15 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
         if (rc) return rc;
-        rc = ensure_ws(M, device, S);
+        rc = ensure_ws(M, device, Sv);
         if (rc) return rc;
+        if (ref_direct && !prm->emit_paths) {
+            rc = ensure_rec(M, device, S);
+            if (rc) return rc;
+            rec = rec_buf(M->dev[device].rec);
+            adjm = adj_buf(M->dev[device].rec, M->dev[device].rec_cap);
+        }
         pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
-        rec = rec_buf(M->dev[device].ws, M->dev[device].ws_cap);
-        adjm = adj_buf(M->dev[device].ws, M->dev[device].ws_cap);
         mg.buf = M->dev[device].map;
         mg.n = M->n;
     }
@@ -1127,7 +1203,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 D.ev_pool.pop_back();
                 D.ev_rec.push_back(ev[i]);
             }
-            D.ev_has3.push_back(prm->cost_mode == PP_COST_COMFORT || !prm->emit_paths ? 1 : 0);
+            D.ev_has3.push_back(!(ref_direct && prm->emit_paths) ? 1 : 0);
         }
     }
     pp_params P = *prm;
@@ -1137,39 +1213,43 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     // K1
     {
         const int threads = 256;
-        const int64_t blocks = (S + threads - 1) / threads;
+        const int64_t blocks = (Sv + threads - 1) / threads;
         const size_t lds = sizeof(double) * 13 * (size_t)mg.n;
         if (timing) (void)hipEventRecord(ev[0], st);
-        hipLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info);
+        hipLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status);
     }
     // K2
     {
-        const int C = 3 * P.n_speeds;
-        const int spb = cands_per_block(C);
-        const int threads = ((spb * C + 63) / 64) * 64;
+        // a block holds SPB whole scenes (all draws: the spline slots are shared by the draws),
+        // or, when a scene has more than 256 candidates, BPS blocks share one scene
+        const int C = Dn * 3 * P.n_speeds;
+        const int spb = C <= 256 ? cands_per_block(C) : 1;
+        const int bps = C <= 256 ? 1 : (C + 255) / 256;
+        const int threads = C <= 256 ? ((spb * C + 63) / 64) * 64 : 256;
         const int nslot = 3 * spb;
         const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
-        const int64_t blocks = (S + spb - 1) / spb;
+        const int64_t blocks = bps == 1 ? (S + spb - 1) / spb : S * bps;
+        if (blocks > 0x7fffffff) return PP_ERR_ARG;
         if (timing) (void)hipEventRecord(ev[1], st);
         if (P.emit_paths) {
-            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
-        } else if (P.cost_mode == PP_COST_REFERENCE) {
-            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
+            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
+        } else if (ref_direct) {
+            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
         } else {
-            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, rec, adjm);
+            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
+            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
         }
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
-    if (P.cost_mode == PP_COST_REFERENCE && !P.emit_paths) {
+    if (ref_direct && !P.emit_paths) {
         const int64_t blocks = (S + 255) / 256;
         hipLaunchKernelGGL(k_emit, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm);
     }
-    // K3 (comfort mode): argmin + winner path (reference mode: k_cand's winner lanes wrote it)
-    if (P.cost_mode == PP_COST_COMFORT) {
+    // K3 (comfort mode, or any mode with draws): argmin + winner path
+    if (!ref_direct) {
         const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
         hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
         hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);

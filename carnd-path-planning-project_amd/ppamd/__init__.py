@@ -54,7 +54,9 @@ class Params(C.Structure):
                 ("relaxed_acc", C.c_double), ("min_relaxed_acc_while_braking", C.c_double),
                 ("maximum_acc", C.c_double), ("max_speed", C.c_double), ("car_length", C.c_double),
                 ("safety_distance", C.c_double), ("keep_distance", C.c_double),
-                ("keep_distance_leeway", C.c_double)]
+                ("keep_distance_leeway", C.c_double), ("n_draws", C.c_int32), ("_pad_mc", C.c_int32),
+                ("noise_seed", C.c_uint64), ("noise_first_scene", C.c_int64),
+                ("noise_pos_sigma", C.c_double), ("noise_vel_sigma", C.c_double)]
 
 
 class SceneInfo(C.Structure):
@@ -77,13 +79,15 @@ assert INFO_DTYPE.itemsize == C.sizeof(SceneInfo)
 class Result(C.Structure):
     _fields_ = [("winner", C.c_void_p), ("n_out", C.c_void_p), ("next_x", C.c_void_p),
                 ("next_y", C.c_void_p), ("cost", C.c_void_p), ("status", C.c_void_p),
-                ("paths", C.c_void_p), ("path_len", C.c_void_p), ("info", C.c_void_p)]
+                ("paths", C.c_void_p), ("path_len", C.c_void_p), ("info", C.c_void_p),
+                ("draw_mean_cost", C.c_void_p)]
 
 
 # exported symbols of include/pp.h (checked by tests/test_capi.py)
 EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_create",
            "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
-           "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read"]
+           "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
+           "pp_mc_gauss"]
 
 
 def _load():
@@ -126,6 +130,8 @@ def _load():
     lib.pp_timing_enable.restype = C.c_int32
     lib.pp_timing_read.argtypes = [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64)]
     lib.pp_timing_read.restype = C.c_int32
+    lib.pp_mc_gauss.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    lib.pp_mc_gauss.restype = C.c_double
     return lib
 
 
@@ -142,13 +148,17 @@ def _check(rc, what):
 
 
 def default_params(n_speeds=5, n_points=50, cost_mode=COST_REFERENCE, emit_paths=False,
-                   speed_offsets=None) -> Params:
+                   speed_offsets=None, n_draws=0, noise_seed=None, noise_first_scene=0) -> Params:
     p = Params()
     lib.pp_params_default(C.byref(p))
     p.n_speeds = n_speeds
     p.n_points = n_points
     p.cost_mode = cost_mode
     p.emit_paths = 1 if emit_paths else 0
+    p.n_draws = n_draws
+    if noise_seed is not None:
+        p.noise_seed = noise_seed
+    p.noise_first_scene = noise_first_scene
     if speed_offsets is not None:
         for i, v in enumerate(speed_offsets):
             p.speed_offsets[i] = float(v)
@@ -260,7 +270,8 @@ def synth_device(m: Map, S, seed=0x5EED0001, first=0, device=0, stream=None, car
 
 
 def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
-    Cn = 3 * prm.n_speeds
+    D = max(prm.n_draws, 1)
+    Cn = D * 3 * prm.n_speeds
     N = prm.n_points
     if xp == "numpy":
         mk = lambda sh, dt: np.zeros(sh, dt)
@@ -275,6 +286,8 @@ def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
     if prm.emit_paths:
         r["paths"] = mk((S, N, Cn, 2), f8)
         r["path_len"] = mk((S, Cn), i4)
+    if D > 1:
+        r["draw_mean_cost"] = mk((S, 3 * prm.n_speeds), f8)
     if info:
         if xp == "numpy":
             r["info"] = np.zeros((S,), INFO_DTYPE)
@@ -286,7 +299,8 @@ def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
 
 def result_struct(r) -> Result:
     R = Result()
-    for k in ["winner", "n_out", "next_x", "next_y", "cost", "status", "paths", "path_len", "info"]:
+    for k in ["winner", "n_out", "next_x", "next_y", "cost", "status", "paths", "path_len", "info",
+              "draw_mean_cost"]:
         setattr(R, k, _ptr(r.get(k)))
     return R
 

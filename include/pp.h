@@ -36,6 +36,7 @@ extern "C" {
 #define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
 #define PP_MAX_POINTS  128  /* horizon N upper bound (reference: 50, src/main.cpp:854,1039)   */
 #define PP_MAX_KNOTS   16   /* spline knots: 9 prev + 1 + 5 control points (src/main.cpp:744) */
+#define PP_MAX_DRAWS   1024 /* Monte-Carlo sensor-noise draws per scene (pp_params.n_draws)   */
 
 /* ---- status codes ------------------------------------------------------------------------ */
 #define PP_OK              0
@@ -108,6 +109,20 @@ typedef struct pp_params {
     double  safety_distance;                /* 2    */
     double  keep_distance;                  /* 10   */
     double  keep_distance_leeway;           /* 0.5  */
+    /* Monte-Carlo sensor noise (BASELINE config 4). n_draws = D > 1
+     * evaluates every scene D times: draw 0 is the scene as given, draw d >= 1 perturbs every
+     * sensor_fusion car j by (sigma_pos g0, sigma_pos g1, sigma_vel g2, sigma_vel g3) added to
+     * (x, y, vx, vy), g = pp_mc_gauss(noise_seed, noise_first_scene + s, d, j, q). Candidates per
+     * scene become C = D * 3 * n_speeds, c = (d * 3 + lane) * n_speeds + k. The per-scene decision
+     * averages each (lane, k) cost over the draws (summed in draw order, then / D) and takes the
+     * first minimum; next_x/next_y are the draw-0 (nominal) trajectory of that (lane, k), winner
+     * = lane * n_speeds + k. emit_paths must be 0 when D > 1. */
+    int32_t n_draws;                        /* 0 or 1: off                                  */
+    int32_t _pad_mc;
+    uint64_t noise_seed;
+    int64_t noise_first_scene;              /* global index of the batch's scene 0 (shards)  */
+    double  noise_pos_sigma;                /* 0.5 m                        */
+    double  noise_vel_sigma;                /* 0.5 m/s                                       */
 } pp_params;
 
 /* ---- optional per-scene diagnostics (the planner's intermediate state) --------------------- */
@@ -126,7 +141,7 @@ typedef struct pp_scene_info {
 } pp_scene_info;
 
 /* ---- results (caller owned; device resident for pp_eval) ---------------------------------- */
-/* C = PP_NUM_LANES * n_speeds, candidate c = lane * n_speeds + k.
+/* C = PP_NUM_LANES * n_speeds (times n_draws for Monte-Carlo), candidate c = lane * n_speeds + k.
  * next_x/next_y: point-major like the batch's prev_x/prev_y, [i * n_scenes + s] (i < n_points;
  * points i >= n_out[s] are 0); cost: [s * C + c];
  * paths (emit_paths): [((s * n_points + i) * C + c) * 2 + {0:x, 1:y}], path_len: [s * C + c]. */
@@ -140,6 +155,8 @@ typedef struct pp_result {
     double*   paths;          /* optional (emit_paths)                                          */
     int32_t*  path_len;       /* optional (emit_paths)                                          */
     pp_scene_info* info;      /* optional                                                       */
+    double*   draw_mean_cost; /* optional (n_draws > 1): [s * 3 * n_speeds + lane * n_speeds + k],
+                                 the draw-averaged cost the decision minimises                  */
 } pp_result;
 
 /* ---- API ----------------------------------------------------------------------------------- */
@@ -188,6 +205,12 @@ int32_t pp_synth_scenes_host(const pp_map* m, uint64_t seed, int64_t first_scene
  * summed milliseconds and launch counts per kernel, and clears the record. */
 int32_t pp_timing_enable(pp_map* m, int32_t device, int32_t enable);
 int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches3);
+
+/* The Monte-Carlo noise generator (host copy of the device code; bit-identical): standard-normal-
+ * like variate q (0..3 -> x, y, vx, vy) of car j in draw d of global scene `scene`. Irwin-Hall of
+ * four 32-bit Philox4x32-10 uniforms (key = seed, counter = {scene, (d*PP_MAX_CARS + j)*4 + q,
+ * 0x4D43}), scaled to unit variance: only exactly rounded arithmetic, no libm. */
+double  pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q);
 
 /* Library version / build info string. */
 const char* pp_version(void);

@@ -514,8 +514,35 @@ typedef struct {
 
 static const uint32_t limit_flag[5] = {0, PP_ST_BRAKE, PP_ST_MAXBRAKE, PP_ST_ADJUST, PP_ST_KEEP};
 
+/* Monte-Carlo sensor noise (build extension, include/pp.h pp_params / pp_mc_gauss): Philox4x32-10
+ * block keyed by the seed, counter {scene, (draw * 16 + car) * 4 + q, 0x4D43}; Irwin-Hall of its
+ * four 32-bit uniforms scaled to unit variance. */
+static double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, int q) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)((draw * 16 + car) * 4 + q), 0x4D43u};
+    for (int r = 0; r < 10; r++) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0], p1 = (uint64_t)0xCD9E8D57u * ctr[2];
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ ctr[1] ^ key[0];
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ ctr[3] ^ key[1];
+        ctr[0] = n0; ctr[1] = (uint32_t)p1; ctr[2] = n2; ctr[3] = (uint32_t)p0;
+        key[0] += 0x9E3779B9u;
+        key[1] += 0xBB67AE85u;
+    }
+    const double k = 1.0 / 4294967296.0;
+    double a = ((double)ctr[0] + 0.5) * k;
+    a += ((double)ctr[1] + 0.5) * k;
+    a += ((double)ctr[2] + 0.5) * k;
+    a += ((double)ctr[3] + 0.5) * k;
+    return (a - 2.0) * 1.7320508075688772;
+}
+
+double ppo_mc_gauss(uint64_t seed, int64_t scene, int draw, int car, int q) {
+    return mc_gauss(seed, (uint64_t)scene, draw, car, q);
+}
+
+/* draw > 0: the sensor-fusion cars carry Monte-Carlo noise (P->n_draws) */
 static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* in, int64_t s,
-                       OPrep* pr) {
+                       int draw, OPrep* pr) {
     const int64_t S = in->n_scenes;
     memset(pr, 0, sizeof(*pr));
     pr->ego_x = in->ego_x[s];
@@ -570,6 +597,13 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
         c.y = in->car_y[ix];
         c.vx = in->car_vx[ix];
         c.vy = in->car_vy[ix];
+        if (draw > 0) {
+            const uint64_t gs = (uint64_t)(P->noise_first_scene + s);
+            c.x += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, j, 0);
+            c.y += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, j, 1);
+            c.vx += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, j, 2);
+            c.vy += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, j, 3);
+        }
         int nwp = 0;
         if (!lane_matching(m, &pr->fr, c.x, c.y, &c.s, &c.d, &c.lane, &nwp)) {
             pr->status |= PP_ST_CAR_UNMATCHED;
@@ -875,47 +909,65 @@ int ppo_map_geometry(const double* wx, const double* wy, int n, double* out10) {
     return 0;
 }
 
-/* Evaluate scenes [s_begin, s_end) of a host batch; outputs indexed by the global scene id. */
+/* Evaluate scenes [s_begin, s_end) of a host batch; outputs indexed by the global scene id.
+ * n_draws = D > 1: every scene is prepared and evaluated D times (draw 0 nominal, draws >= 1 with
+ * car noise); cost[s * C + d * Cv + c]; decision = first minimum of the draw-averaged cost (sum in
+ * draw order, / D); next_x/next_y = that candidate on the nominal scene. */
 int ppo_eval_range(const double* wx, const double* wy, int n_wp, const pp_scene_batch* in,
                    const pp_params* P, pp_result* out, int64_t s_begin, int64_t s_end) {
     if (!in || !P || !out || P->n_points <= PP_PREV_KEEP || P->n_points > PP_MAX_POINTS || P->n_speeds < 1 ||
-        P->n_speeds > PP_MAX_SPEEDS || in->car_stride > PP_MAX_CARS)
+        P->n_speeds > PP_MAX_SPEEDS || in->car_stride > PP_MAX_CARS || P->n_draws < 0 || P->n_draws > PP_MAX_DRAWS)
         return -1;
+    const int D = P->n_draws > 1 ? P->n_draws : 1;
+    if (D > 1 && out->paths) return -1;
     OMap m;
     if (n_wp < 2 || omap_init(&m, wx, wy, n_wp)) return -1;
-    const int NS = P->n_speeds, C = PP_NUM_LANES * NS, N = P->n_points;
+    const int NS = P->n_speeds, Cv = PP_NUM_LANES * NS, C = D * Cv, N = P->n_points;
     double gx[PP_MAX_POINTS], gy[PP_MAX_POINTS];
+    double* dcost = (double*)malloc(sizeof(double) * (size_t)C);
     for (int64_t s = s_begin; s < s_end; s++) {
-        OPrep pr;
-        prep_scene(&m, P, in, s, &pr);
-        uint32_t status = pr.status;
+        OPrep pr, pr0;
+        uint32_t status = 0;
+        for (int d = 0; d < D; d++) {
+            prep_scene(&m, P, in, s, d, &pr);
+            if (d == 0) pr0 = pr;
+            status |= pr.status;
+            for (int c = 0; c < Cv; c++) {
+                int L = c / NS, k = c % NS;
+                double v = cand_speed(P, pr.ego_speed, k);
+                OSC sc = make_sc(P, &pr, L, v);
+                OStats st;
+                int ng = build_traj(&m, P, &pr, L, sc, N, gx, gy, &st);
+                int isn;
+                double cost = cand_cost(P, &pr, L, v, ng, &st, &isn);
+                status |= (st.fallback ? PP_ST_FALLBACK : 0) | (st.trunc ? PP_ST_SPLINE_TRUNC : 0) |
+                          (isn ? PP_ST_NAN : 0) | (st.override_hit ? PP_ST_ACC_OVERRIDE : 0) |
+                          (st.curv_hit ? PP_ST_CURV_ADJUST : 0);
+                dcost[d * Cv + c] = cost;
+                if (out->cost) out->cost[s * C + d * Cv + c] = cost;
+                if (out->paths) {
+                    for (int i = 0; i < N; i++) {
+                        double px = NAN, py = NAN;
+                        if (i < pr.K) { px = pr.prev[i].x; py = pr.prev[i].y; }
+                        else if (i - pr.K < ng) { px = gx[i - pr.K]; py = gy[i - pr.K]; }
+                        out->paths[((s * N + i) * C + c) * 2 + 0] = px;
+                        out->paths[((s * N + i) * C + c) * 2 + 1] = py;
+                    }
+                }
+                if (out->path_len) out->path_len[s * C + c] = pr.K + ng;
+            }
+        }
         int best = 0;
         double best_cost = 0;
-        for (int c = 0; c < C; c++) {
-            int L = c / NS, k = c % NS;
-            double v = cand_speed(P, pr.ego_speed, k);
-            OSC sc = make_sc(P, &pr, L, v);
-            OStats st;
-            int ng = build_traj(&m, P, &pr, L, sc, N, gx, gy, &st);
-            int isn;
-            double cost = cand_cost(P, &pr, L, v, ng, &st, &isn);
-            status |= (st.fallback ? PP_ST_FALLBACK : 0) | (st.trunc ? PP_ST_SPLINE_TRUNC : 0) |
-                      (isn ? PP_ST_NAN : 0) | (st.override_hit ? PP_ST_ACC_OVERRIDE : 0) |
-                      (st.curv_hit ? PP_ST_CURV_ADJUST : 0);
-            if (out->cost) out->cost[s * C + c] = cost;
-            if (c == 0 || cost < best_cost) { best = c; best_cost = cost; }
-            if (out->paths) {
-                for (int i = 0; i < N; i++) {
-                    double px = NAN, py = NAN;
-                    if (i < pr.K) { px = pr.prev[i].x; py = pr.prev[i].y; }
-                    else if (i - pr.K < ng) { px = gx[i - pr.K]; py = gy[i - pr.K]; }
-                    out->paths[((s * N + i) * C + c) * 2 + 0] = px;
-                    out->paths[((s * N + i) * C + c) * 2 + 1] = py;
-                }
-            }
-            if (out->path_len) out->path_len[s * C + c] = pr.K + ng;
+        for (int c = 0; c < Cv; c++) {
+            double sum = dcost[c];
+            for (int d = 1; d < D; d++) sum += dcost[d * Cv + c];
+            const double mean = sum / D;
+            if (D > 1 && out->draw_mean_cost) out->draw_mean_cost[s * Cv + c] = mean;
+            if (c == 0 || mean < best_cost) { best = c; best_cost = mean; }
         }
-        /* winner path: re-run the winning candidate */
+        pr = pr0;
+        /* winner path: re-run the winning candidate on the nominal scene */
         {
             int L = best / NS, k = best % NS;
             double v = cand_speed(P, pr.ego_speed, k);
@@ -945,6 +997,7 @@ int ppo_eval_range(const double* wx, const double* wy, int n_wp, const pp_scene_
             I->lane_open_mask = pr.open_mask; I->n_matched_cars = pr.nmatched; I->in_lane_car = pr.in_id;
         }
     }
+    free(dcost);
     omap_free(&m);
     return 0;
 }

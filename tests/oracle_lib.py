@@ -37,7 +37,40 @@ def load_oracle():
     lib.ppo_map_geometry.argtypes = [_dp, _dp, C.c_int, _dp]
     lib.ppo_map_geometry.restype = C.c_int
     lib.ppo_struct_sizes.argtypes = [C.POINTER(C.c_int64)]
+    lib.ppo_mc_gauss.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int]
+    lib.ppo_mc_gauss.restype = C.c_double
     return lib
+
+
+def noisy_scenes(olib, scenes, prm, draw, first=0):
+    """Materialise draw `draw` of a Monte-Carlo batch on the host: every car's (x, y, vx, vy) plus
+    sigma * g (include/pp.h pp_params; same operations and order as the kernels)."""
+    out = {k: np.array(v, copy=True) for k, v in scenes.items()}
+    if draw == 0:
+        return out
+    S = out["ego_x"].shape[0]
+    J = out["car_x"].shape[0]
+    g = np.zeros((4, J, S))
+    for s in range(S):
+        for j in range(J):
+            for q in range(4):
+                g[q, j, s] = olib.ppo_mc_gauss(prm.noise_seed, prm.noise_first_scene + first + s, draw, j, q)
+    out["car_x"] = out["car_x"] + prm.noise_pos_sigma * g[0]
+    out["car_y"] = out["car_y"] + prm.noise_pos_sigma * g[1]
+    out["car_vx"] = out["car_vx"] + prm.noise_vel_sigma * g[2]
+    out["car_vy"] = out["car_vy"] + prm.noise_vel_sigma * g[3]
+    return out
+
+
+def draw_decision(cost, D, Cv):
+    """Per-scene decision of the Monte-Carlo mode: first minimum of the draw-averaged cost (sum in
+    draw order, then / D). Returns (mean [S, Cv], winner [S])."""
+    c = cost.reshape(cost.shape[0], D, Cv)
+    acc = c[:, 0, :].copy()
+    for d in range(1, D):
+        acc = acc + c[:, d, :]
+    mean = acc / D
+    return mean, np.argmin(mean, axis=1).astype(np.int32)
 
 
 def load_ref():

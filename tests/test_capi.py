@@ -14,7 +14,7 @@ HEADER = os.path.join(oracle_lib.REPO, "include", "pp.h")
 
 def declared_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|void|const char\*)\s+(pp_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|void|double|const char\*)\s+(pp_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_symbols_exported():
