@@ -118,25 +118,53 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
     int nmatched = 0;
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
-    for (int j = 0; j < ncar; j++) {
-        const int64_t ix = (int64_t)j * S + s;
-        const int id = in.car_id[ix];
-        double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
-        if (draw > 0) {                     // Monte-Carlo sensor noise (include/pp.h pp_params)
-            const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
-            cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 0);
-            cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 1);
-            cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 2);
-            cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 3);
+    // Without a car table: the frame's rows in order (ascending ids). With one (the reference's
+    // persistent std::map): ids 0..PP_MAX_CARS-1 in order, each either reported this frame
+    // (re-matched; slot overwritten, or erased when matching fails, src/main.cpp:1329-1348) or
+    // taken from its stale slot.
+    const bool tab = in.tab_valid != nullptr;
+    const int iters = tab ? PP_MAX_CARS : ncar;
+    int p = 0;                              // next unread row (table mode)
+    for (int it = 0; it < iters; it++) {
+        int row = it;
+        if (tab) {
+            while (p < ncar && in.car_id[(int64_t)p * S + s] < it) p++;     // ids must ascend
+            row = (p < ncar && in.car_id[(int64_t)p * S + s] == it) ? p++ : -1;
         }
-        double cs, cd;
-        int clane = 0, nwp = 0;
-        if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
-            status |= PP_ST_CAR_UNMATCHED;
-            continue;
+        int id;
+        double cx, cy, cvx, cvy, cs, cd, cvs, cvd;
+        int clane = 0;
+        const int64_t tix = (int64_t)it * S + s;
+        if (row >= 0) {
+            const int64_t ix = (int64_t)row * S + s;
+            id = in.car_id[ix];
+            cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
+            if (draw > 0) {                     // Monte-Carlo sensor noise (include/pp.h pp_params)
+                const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+                cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 0);
+                cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 1);
+                cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 2);
+                cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
+            }
+            int nwp = 0;
+            if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
+                status |= PP_ST_CAR_UNMATCHED;
+                if (tab) in.tab_valid[tix] = 0;
+                continue;
+            }
+            project_speed(m, cvx, cvy, nwp, cvs, cvd);
+            if (tab) {
+                in.tab_valid[tix] = 1; in.tab_lane[tix] = clane;
+                in.tab_s[tix] = cs; in.tab_d[tix] = cd; in.tab_vs[tix] = cvs; in.tab_vd[tix] = cvd;
+                in.tab_vx[tix] = cvx; in.tab_vy[tix] = cvy;
+            }
+        } else {
+            if (!in.tab_valid[tix]) continue;
+            id = it;
+            clane = in.tab_lane[tix];
+            cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
+            cvx = in.tab_vx[tix]; cvy = in.tab_vy[tix];
         }
-        double cvs, cvd;
-        project_speed(m, cvx, cvy, nwp, cvs, cvd);
         nmatched++;
         // planner (src/main.cpp:379-444)
         const double sp = cs + cvs * dt0;
@@ -875,6 +903,99 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
 }
 
 // ------------------------------------------------------------------------------------------------
+// closed-loop rollout: the simulator shim (include/pp.h pp_rollout). One lane per scene: log the
+// frame, drive `consume` points of the plan, advance the traffic, report the cars in range.
+// ------------------------------------------------------------------------------------------------
+struct SimArgs {
+    int consume;
+    double range2;
+    int frame;
+    pp_rollout_log log;
+};
+
+__global__ __launch_bounds__(256) void k_sim(ppsynth::LaneTables LT, pp_scene_batch in,
+                                             ppsynth::TrafficV tr, pp_params P, pp_result out, SimArgs A) {
+    const int64_t S = in.n_scenes;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int N = P.n_points;
+    const int n_out = out.n_out[s];
+    const int T = out.winner[s] / P.n_speeds;
+    double* ex = (double*)in.ego_x;
+    double* ey = (double*)in.ego_y;
+    double* eyaw = (double*)in.ego_yaw_deg;
+    double* espd = (double*)in.ego_speed_mph;
+    double* px = (double*)in.prev_x;
+    double* py = (double*)in.prev_y;
+    const double x0 = ex[s], y0 = ey[s];
+    // frame record (the telemetry this frame was planned from + its plan)
+    const int64_t fs = (int64_t)A.frame * S + s;
+    if (A.log.ego_x) A.log.ego_x[fs] = x0;
+    if (A.log.ego_y) A.log.ego_y[fs] = y0;
+    if (A.log.ego_speed_mph) A.log.ego_speed_mph[fs] = espd[s];
+    if (A.log.target_lane) A.log.target_lane[fs] = T;
+    if (A.log.winner) A.log.winner[fs] = out.winner[s];
+    if (A.log.n_out) A.log.n_out[fs] = n_out;
+    if (A.log.status) A.log.status[fs] = out.status[s];
+    if (A.log.n_cars) A.log.n_cars[fs] = in.n_cars[s];
+    if (A.log.plan_x) {
+        for (int i = 0; i < N; i++) {
+            A.log.plan_x[((int64_t)A.frame * N + i) * S + s] = out.next_x[(int64_t)i * S + s];
+            A.log.plan_y[((int64_t)A.frame * N + i) * S + s] = out.next_y[(int64_t)i * S + s];
+        }
+    }
+    // ego: drive kk points; speed and yaw from the last driven step
+    const int kk = n_out < A.consume ? n_out : A.consume;
+    double nx = x0, ny = y0, qx = x0, qy = y0;
+    if (kk >= 1) { nx = out.next_x[(int64_t)(kk - 1) * S + s]; ny = out.next_y[(int64_t)(kk - 1) * S + s]; }
+    if (kk >= 2) { qx = out.next_x[(int64_t)(kk - 2) * S + s]; qy = out.next_y[(int64_t)(kk - 2) * S + s]; }
+    const double dx = nx - qx, dy = ny - qy;
+    const double dist = sqrt(dx * dx + dy * dy);
+    ex[s] = nx; ey[s] = ny;
+    espd[s] = dist * 50 * 2.237;
+    if (dist > 0) eyaw[s] = atan2(dy, dx) * 180.0 / kPi;
+    const int np = n_out - kk;
+    for (int i = 0; i < PP_PREV_KEEP; i++) {
+        const bool ok = i < np;
+        px[(int64_t)i * S + s] = ok ? out.next_x[(int64_t)(kk + i) * S + s] : 0.0;
+        py[(int64_t)i * S + s] = ok ? out.next_y[(int64_t)(kk + i) * S + s] : 0.0;
+    }
+    ((int32_t*)in.n_prev)[s] = np;
+    ((int32_t*)in.prev_target_lane)[s] = T;
+    // traffic: advance, then report the cars within range, ascending id
+    int nc = 0;
+    for (int j = 0; j < tr.n; j++) {
+        const int64_t tx = (int64_t)j * S + s;
+        const int lane = tr.lane[tx];
+        int seg = tr.seg[tx];
+        double t = tr.t[tx];
+        const double v = tr.v[tx];
+        ppsynth::lane_advance(LT, lane, &seg, &t, v * 0.02 * A.consume);
+        tr.seg[tx] = seg; tr.t[tx] = t;
+        double cx, cy, cvx, cvy;
+        ppsynth::traffic_car(LT, lane, seg, t, tr.off[tx], v, &cx, &cy, &cvx, &cvy);
+        const double rx = cx - nx, ry = cy - ny;
+        if (rx * rx + ry * ry <= A.range2 && nc < in.car_stride) {
+            const int64_t ix = (int64_t)nc * S + s;
+            ((int32_t*)in.car_id)[ix] = j;
+            ((double*)in.car_x)[ix] = cx; ((double*)in.car_y)[ix] = cy;
+            ((double*)in.car_vx)[ix] = cvx; ((double*)in.car_vy)[ix] = cvy;
+            nc++;
+        }
+    }
+    ((int32_t*)in.n_cars)[s] = nc;
+}
+
+__global__ __launch_bounds__(256) void k_synth_traffic(ppsynth::LaneTables T, uint64_t seed, int64_t first,
+                                                       ppsynth::OutBatch o, ppsynth::TrafficV tr, pp_scene_batch tb) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= o.S) return;
+    ppsynth::synth_scene(T, seed, first + s, s, o, &tr);
+    if (tb.tab_valid)
+        for (int j = 0; j < PP_MAX_CARS; j++) tb.tab_valid[(int64_t)j * o.S + s] = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
 // scene synthesis
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_synth(ppsynth::LaneTables T, uint64_t seed, int64_t first,
@@ -902,6 +1023,11 @@ struct DevState {
     void* rec = nullptr;          // reference-mode winner record (per scene)
     int64_t rec_cap = 0;
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
+    bool table_reset = true;      // pp_plan_frame's persistent car table must be cleared
+    struct PlanTab {              // pp_plan_frame's car table (host copy between frames)
+        double s[PP_MAX_CARS], d[PP_MAX_CARS], vs[PP_MAX_CARS], vd[PP_MAX_CARS], vx[PP_MAX_CARS], vy[PP_MAX_CARS];
+        int32_t valid[PP_MAX_CARS], lane[PP_MAX_CARS];
+    } plan_tab;
     bool timing = false;          // pp_timing_enable
     std::vector<hipEvent_t> ev_pool;
     std::vector<hipEvent_t> ev_rec; // groups of 4: before k_prep, after k_prep, after k_cand, after k_winner
@@ -985,6 +1111,30 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
             t[4 * 3 * n + r * n + i] = (lcy[r * n + i] - lcy[r * n + p]) / len;
         }
     return PP_OK;
+}
+
+ppsynth::OutBatch out_batch(const pp_scene_batch* b) {
+    ppsynth::OutBatch o;
+    o.S = b->n_scenes;
+    o.ego_x = (double*)b->ego_x; o.ego_y = (double*)b->ego_y;
+    o.ego_yaw_deg = (double*)b->ego_yaw_deg; o.ego_speed_mph = (double*)b->ego_speed_mph;
+    o.prev_x = (double*)b->prev_x; o.prev_y = (double*)b->prev_y;
+    o.n_prev = (int32_t*)b->n_prev; o.prev_target_lane = (int32_t*)b->prev_target_lane;
+    o.n_cars = (int32_t*)b->n_cars; o.car_id = (int32_t*)b->car_id;
+    o.car_x = (double*)b->car_x; o.car_y = (double*)b->car_y;
+    o.car_vx = (double*)b->car_vx; o.car_vy = (double*)b->car_vy;
+    return o;
+}
+
+bool traffic_ok(const pp_traffic* t, const pp_scene_batch* b) {
+    return t && b && t->n_cars >= 0 && t->n_cars <= PP_MAX_CARS && t->lane && t->seg && t->t &&
+           t->offset && t->speed;
+}
+
+ppsynth::TrafficV traffic_view(const pp_traffic* t, int64_t S) {
+    ppsynth::TrafficV v;
+    v.S = S; v.n = t->n_cars; v.lane = t->lane; v.seg = t->seg; v.t = t->t; v.off = t->offset; v.v = t->speed;
+    return v;
 }
 
 ppsynth::LaneTables lane_tables(const double* t, int n) {
@@ -1158,6 +1308,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     if (!out->winner || !out->n_out || !out->next_x || !out->next_y || !out->cost || !out->status)
         return PP_ERR_ARG;
     if (prm->emit_paths && !out->paths) return PP_ERR_ARG;
+    if (in->tab_valid && (!in->tab_lane || !in->tab_s || !in->tab_d || !in->tab_vs || !in->tab_vd ||
+                          !in->tab_vx || !in->tab_vy || prm->n_draws > 1))
+        return PP_ERR_ARG;
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)hip_stream;
     const int64_t S = in->n_scenes;
@@ -1303,15 +1456,7 @@ int32_t pp_synth_scenes(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_
         if (rc) return rc;
         T = lane_tables(M->dev[device].lanetab, M->n);
     }
-    ppsynth::OutBatch o;
-    o.S = out->n_scenes;
-    o.ego_x = (double*)out->ego_x; o.ego_y = (double*)out->ego_y;
-    o.ego_yaw_deg = (double*)out->ego_yaw_deg; o.ego_speed_mph = (double*)out->ego_speed_mph;
-    o.prev_x = (double*)out->prev_x; o.prev_y = (double*)out->prev_y;
-    o.n_prev = (int32_t*)out->n_prev; o.prev_target_lane = (int32_t*)out->prev_target_lane;
-    o.n_cars = (int32_t*)out->n_cars; o.car_id = (int32_t*)out->car_id;
-    o.car_x = (double*)out->car_x; o.car_y = (double*)out->car_y;
-    o.car_vx = (double*)out->car_vx; o.car_vy = (double*)out->car_vy;
+    const ppsynth::OutBatch o = out_batch(out);
     const int threads = 256;
     const int64_t blocks = (o.S + threads - 1) / threads;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)hip_stream, T, seed, first_scene, o);
@@ -1322,16 +1467,91 @@ int32_t pp_synth_scenes(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_
 int32_t pp_synth_scenes_host(const pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* out) {
     if (!M || !out || out->n_scenes < 0 || first_scene < 0 || out->car_stride < ppsynth::kSynthCars) return PP_ERR_ARG;
     const ppsynth::LaneTables T = lane_tables(M->lanetab.data(), M->n);
-    ppsynth::OutBatch o;
-    o.S = out->n_scenes;
-    o.ego_x = (double*)out->ego_x; o.ego_y = (double*)out->ego_y;
-    o.ego_yaw_deg = (double*)out->ego_yaw_deg; o.ego_speed_mph = (double*)out->ego_speed_mph;
-    o.prev_x = (double*)out->prev_x; o.prev_y = (double*)out->prev_y;
-    o.n_prev = (int32_t*)out->n_prev; o.prev_target_lane = (int32_t*)out->prev_target_lane;
-    o.n_cars = (int32_t*)out->n_cars; o.car_id = (int32_t*)out->car_id;
-    o.car_x = (double*)out->car_x; o.car_y = (double*)out->car_y;
-    o.car_vx = (double*)out->car_vx; o.car_vy = (double*)out->car_vy;
+    const ppsynth::OutBatch o = out_batch(out);
     for (int64_t s = 0; s < o.S; s++) ppsynth::synth_scene(T, seed, first_scene + s, s, o);
+    return PP_OK;
+}
+
+int32_t pp_synth_traffic(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* tel,
+                         pp_traffic* out, int32_t device, void* hip_stream) {
+    if (!M || !tel || device < 0 || device >= kMaxDev || tel->n_scenes < 0 || first_scene < 0 ||
+        tel->car_stride < ppsynth::kSynthCars || !traffic_ok(out, tel))
+        return PP_ERR_ARG;
+    if (tel->n_scenes == 0) return PP_OK;
+    DeviceGuard g(device);
+    ppsynth::LaneTables T;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        const int rc = dev_init(M, device);
+        if (rc) return rc;
+        T = lane_tables(M->dev[device].lanetab, M->n);
+    }
+    out->n_cars = ppsynth::kSynthCars;
+    const ppsynth::OutBatch o = out_batch(tel);
+    const int64_t blocks = (o.S + 255) / 256;
+    hipLaunchKernelGGL(k_synth_traffic, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)hip_stream, T,
+                       seed, first_scene, o, traffic_view(out, o.S), *tel);
+    if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+    return PP_OK;
+}
+
+int32_t pp_synth_traffic_host(const pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* tel,
+                              pp_traffic* out) {
+    if (!M || !tel || tel->n_scenes < 0 || first_scene < 0 || tel->car_stride < ppsynth::kSynthCars ||
+        !traffic_ok(out, tel))
+        return PP_ERR_ARG;
+    const ppsynth::LaneTables T = lane_tables(M->lanetab.data(), M->n);
+    out->n_cars = ppsynth::kSynthCars;
+    const ppsynth::OutBatch o = out_batch(tel);
+    const ppsynth::TrafficV tv = traffic_view(out, o.S);
+    for (int64_t s = 0; s < o.S; s++) {
+        ppsynth::synth_scene(T, seed, first_scene + s, s, o, &tv);
+        if (tel->tab_valid)
+            for (int j = 0; j < PP_MAX_CARS; j++) tel->tab_valid[(int64_t)j * o.S + s] = 0;
+    }
+    return PP_OK;
+}
+
+int32_t pp_rollout(pp_map* M, pp_scene_batch* tel, pp_traffic* traffic, const pp_params* prm,
+                   const pp_rollout_cfg* cfg, pp_result* res, pp_rollout_log* log, int32_t device,
+                   void* hip_stream) {
+    if (!M || !tel || !prm || !cfg || !res || device < 0 || device >= kMaxDev || !traffic_ok(traffic, tel))
+        return PP_ERR_ARG;
+    if (cfg->n_frames < 0 || cfg->consume < 1 || !(cfg->sensor_range >= 0) || prm->n_draws > 1 ||
+        prm->emit_paths || !tel->tab_valid || !tel->tab_lane || !tel->tab_s || !tel->tab_d ||
+        !tel->tab_vs || !tel->tab_vd || !tel->tab_vx || !tel->tab_vy || tel->car_stride < traffic->n_cars)
+        return PP_ERR_ARG;
+    if (log && log->plan_x && !log->plan_y) return PP_ERR_ARG;
+    if (tel->n_scenes == 0 || cfg->n_frames == 0) return PP_OK;
+    DeviceGuard g(device);
+    ppsynth::LaneTables T;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        const int rc = dev_init(M, device);
+        if (rc) return rc;
+        T = lane_tables(M->dev[device].lanetab, M->n);
+    }
+    SimArgs A;
+    A.consume = cfg->consume;
+    A.range2 = cfg->sensor_range * cfg->sensor_range;
+    if (log) A.log = *log; else memset(&A.log, 0, sizeof(A.log));
+    const ppsynth::TrafficV tv = traffic_view(traffic, tel->n_scenes);
+    const int64_t blocks = (tel->n_scenes + 255) / 256;
+    for (int f = 0; f < cfg->n_frames; f++) {
+        const int rc = pp_eval(M, tel, prm, res, device, hip_stream);
+        if (rc != PP_OK) return rc;
+        A.frame = f;
+        hipLaunchKernelGGL(k_sim, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)hip_stream, T, *tel,
+                           tv, *prm, *res, A);
+        if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+    }
+    return PP_OK;
+}
+
+int32_t pp_plan_reset(pp_map* M, int32_t device) {
+    if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
+    std::lock_guard<std::mutex> lk(M->mu);
+    M->dev[device].table_reset = true;
     return PP_OK;
 }
 
@@ -1363,9 +1583,13 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         double ego[4], px[PP_PREV_KEEP], py[PP_PREV_KEEP], cx[PP_MAX_CARS], cy[PP_MAX_CARS],
             cvx[PP_MAX_CARS], cvy[PP_MAX_CARS];
         double nx[N], ny[N], cost[3];
+        DevState::PlanTab tab;
         int32_t nprev, ptl, ncars, cid[PP_MAX_CARS], winner, nout;
         uint32_t status;
     };
+    // the reference's car table persists across frames when every id fits a slot
+    bool use_tab = true;
+    for (const Row& r : rows) if (r.id < 0 || r.id >= PP_MAX_CARS) use_tab = false;
     Frame h;
     memset(&h, 0, sizeof(h));
     h.ego[0] = ego_x; h.ego[1] = ego_y; h.ego[2] = ego_yaw_deg; h.ego[3] = ego_speed_mph;
@@ -1382,6 +1606,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         if (rc) return rc;
         if (!M->dev[device].frame && hipMalloc(&M->dev[device].frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
         d = (Frame*)M->dev[device].frame;
+        DevState& D = M->dev[device];
+        if (D.table_reset) { memset(&D.plan_tab, 0, sizeof(D.plan_tab)); D.table_reset = false; }
+        h.tab = D.plan_tab;
     }
     if (hipMemcpy(d, &h, sizeof(Frame), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
     pp_scene_batch B;
@@ -1390,6 +1617,10 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     B.ego_x = &d->ego[0]; B.ego_y = &d->ego[1]; B.ego_yaw_deg = &d->ego[2]; B.ego_speed_mph = &d->ego[3];
     B.prev_x = d->px; B.prev_y = d->py; B.n_prev = &d->nprev; B.prev_target_lane = &d->ptl;
     B.n_cars = &d->ncars; B.car_id = d->cid; B.car_x = d->cx; B.car_y = d->cy; B.car_vx = d->cvx; B.car_vy = d->cvy;
+    if (use_tab) {
+        B.tab_valid = d->tab.valid; B.tab_lane = d->tab.lane; B.tab_s = d->tab.s; B.tab_d = d->tab.d;
+        B.tab_vs = d->tab.vs; B.tab_vd = d->tab.vd; B.tab_vx = d->tab.vx; B.tab_vy = d->tab.vy;
+    }
     pp_params P;
     pp_params_default(&P);
     P.n_speeds = 1;
@@ -1406,6 +1637,10 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     if (rc == PP_OK && hipMemcpy(&hi, dinfo, sizeof(hi), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
     (void)hipFree(dinfo);
     if (rc != PP_OK) return rc;
+    if (use_tab) {
+        std::lock_guard<std::mutex> lk(M->mu);
+        M->dev[device].plan_tab = h.tab;
+    }
     *n_out = h.nout;
     for (int i = 0; i < h.nout && i < N; i++) { next_x[i] = h.nx[i]; next_y[i] = h.ny[i]; }
     *target_lane = hi.target_lane;

@@ -102,7 +102,8 @@ struct Rng {
 // Walk `dist` metres (signed) along lane `lane` from segment `seg` (1..n; segment i ends at wp i)
 // at fraction t. Returns the point and the segment tangent at the arrival point.
 PP_HD inline void lane_walk(const LaneTables& T, int lane, int seg, double t, double dist,
-                            double* px, double* py, double* ux, double* uy) {
+                            double* px, double* py, double* ux, double* uy,
+                            int* oseg = nullptr, double* ot = nullptr) {
     const int n = T.n;
     int i = seg;
     for (int it = 0; it < 4 * n + 8; it++) {
@@ -124,6 +125,46 @@ PP_HD inline void lane_walk(const LaneTables& T, int lane, int seg, double t, do
     *py = ay + (by - ay) * t;
     *ux = T.tan_x[lane * n + i];
     *uy = T.tan_y[lane * n + i];
+    if (oseg) { *oseg = i; *ot = t; }
+}
+
+// The rollout simulator's traffic (include/pp.h pp_traffic): car j of scene s at [j * S + s].
+struct TrafficV {
+    int64_t S;
+    int n;
+    int32_t *lane, *seg;
+    double *t, *off, *v;
+};
+
+// Car on lane `lane` at fraction t of segment `seg`, lateral offset `off`, speed v along the lane:
+// telemetry position and velocity (the same formulas as synth_scene's cars, lateral speed 0).
+PP_HD inline void traffic_car(const LaneTables& T, int lane, int seg, double t, double off, double v,
+                              double* x, double* y, double* vx, double* vy) {
+    const int n = T.n;
+    const int ip = (seg == 0) ? n - 1 : seg - 1;
+    const double ax = T.lc_x[lane * n + ip], ay = T.lc_y[lane * n + ip];
+    const double bx = T.lc_x[lane * n + seg], by = T.lc_y[lane * n + seg];
+    const double px = ax + (bx - ax) * t, py = ay + (by - ay) * t;
+    const double ux = T.tan_x[lane * n + seg], uy = T.tan_y[lane * n + seg];
+    *x = px + uy * off;
+    *y = py - ux * off;
+    *vx = ux * v;
+    *vy = uy * v;
+}
+
+// Advance (seg, t) by dist >= 0 metres along the lane polyline (lane_walk's forward branch).
+PP_HD inline void lane_advance(const LaneTables& T, int lane, int* seg, double* t, double dist) {
+    const int n = T.n;
+    int i = *seg;
+    double tt = *t;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        const double L = T.seg_len[lane * n + i];
+        const double rem = (1.0 - tt) * L;
+        if (dist <= rem || it == 4 * n + 7) { tt = tt + dist / L; break; }
+        dist -= rem; tt = 0.0; i = (i + 1 == n) ? 0 : i + 1;
+    }
+    *seg = i;
+    *t = tt;
 }
 
 // Writable view of one batch (pointers into SoA arrays, see include/pp.h index conventions).
@@ -139,7 +180,7 @@ constexpr int kSynthCars = 12;
 // Generates scene `local` of the batch from global index `g`. yaw uses atan2 (the one
 // transcendental); everything else is exact arithmetic on the lane tables.
 PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int64_t local,
-                              const OutBatch& o) {
+                              const OutBatch& o, const TrafficV* traffic = nullptr) {
     Rng r(seed, (uint64_t)g);
     const int64_t S = o.S;
     const int n = T.n;
@@ -190,7 +231,14 @@ PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int
         const double cs = r.uni(5.0, 25.0);
         const double cvd = 0.3 * r.gauss();
         double px, py, ux, uy;
-        lane_walk(T, cl, seg, t, ds, &px, &py, &ux, &uy);
+        int cseg;
+        double ct;
+        lane_walk(T, cl, seg, t, ds, &px, &py, &ux, &uy, &cseg, &ct);
+        if (traffic) {
+            const int64_t tx = (int64_t)j * traffic->S + local;
+            traffic->lane[tx] = cl; traffic->seg[tx] = cseg; traffic->t[tx] = ct;
+            traffic->off[tx] = cd; traffic->v[tx] = cs;
+        }
         o.car_id[ix] = j;
         o.car_x[ix] = px + uy * cd;
         o.car_y[ix] = py - ux * cd;

@@ -45,7 +45,30 @@ class SceneBatch(C.Structure):
                 ("ego_speed_mph", C.c_void_p), ("prev_x", C.c_void_p), ("prev_y", C.c_void_p),
                 ("n_prev", C.c_void_p), ("prev_target_lane", C.c_void_p), ("n_cars", C.c_void_p),
                 ("car_id", C.c_void_p), ("car_x", C.c_void_p), ("car_y", C.c_void_p),
-                ("car_vx", C.c_void_p), ("car_vy", C.c_void_p)]
+                ("car_vx", C.c_void_p), ("car_vy", C.c_void_p),
+                ("tab_valid", C.c_void_p), ("tab_lane", C.c_void_p), ("tab_s", C.c_void_p),
+                ("tab_d", C.c_void_p), ("tab_vs", C.c_void_p), ("tab_vd", C.c_void_p),
+                ("tab_vx", C.c_void_p), ("tab_vy", C.c_void_p)]
+
+TABLE_FIELDS_I = ["tab_valid", "tab_lane"]
+TABLE_FIELDS_F = ["tab_s", "tab_d", "tab_vs", "tab_vd", "tab_vx", "tab_vy"]
+
+
+class Traffic(C.Structure):
+    _fields_ = [("n_cars", C.c_int32), ("_pad", C.c_int32), ("lane", C.c_void_p), ("seg", C.c_void_p),
+                ("t", C.c_void_p), ("offset", C.c_void_p), ("speed", C.c_void_p)]
+
+
+class RolloutCfg(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("consume", C.c_int32), ("sensor_range", C.c_double)]
+
+
+LOG_FIELDS = [("ego_x", "f8"), ("ego_y", "f8"), ("ego_speed_mph", "f8"), ("target_lane", "i4"),
+              ("winner", "i4"), ("n_out", "i4"), ("status", "u4"), ("n_cars", "i4")]
+
+
+class RolloutLog(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k, _ in LOG_FIELDS] + [("plan_x", C.c_void_p), ("plan_y", C.c_void_p)]
 
 
 class Params(C.Structure):
@@ -87,7 +110,7 @@ class Result(C.Structure):
 EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_create",
            "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
-           "pp_mc_gauss"]
+           "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset"]
 
 
 def _load():
@@ -132,6 +155,18 @@ def _load():
     lib.pp_timing_read.restype = C.c_int32
     lib.pp_mc_gauss.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32]
     lib.pp_mc_gauss.restype = C.c_double
+    lib.pp_rollout.argtypes = [C.c_void_p, C.POINTER(SceneBatch), C.POINTER(Traffic), C.POINTER(Params),
+                               C.POINTER(RolloutCfg), C.POINTER(Result), C.POINTER(RolloutLog), C.c_int32,
+                               C.c_void_p]
+    lib.pp_rollout.restype = C.c_int32
+    lib.pp_synth_traffic.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, C.POINTER(SceneBatch),
+                                     C.POINTER(Traffic), C.c_int32, C.c_void_p]
+    lib.pp_synth_traffic.restype = C.c_int32
+    lib.pp_synth_traffic_host.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, C.POINTER(SceneBatch),
+                                          C.POINTER(Traffic)]
+    lib.pp_synth_traffic_host.restype = C.c_int32
+    lib.pp_plan_reset.argtypes = [C.c_void_p, C.c_int32]
+    lib.pp_plan_reset.restype = C.c_int32
     return lib
 
 
@@ -247,7 +282,99 @@ def scene_struct(d) -> SceneBatch:
     b.car_stride = int(d["car_id"].shape[0])
     for k in SCENE_FIELDS_F + SCENE_FIELDS_I + CAR_FIELDS_F + ["prev_x", "prev_y", "car_id"]:
         setattr(b, k, _ptr(d[k]))
+    for k in TABLE_FIELDS_I + TABLE_FIELDS_F:
+        setattr(b, k, _ptr(d.get(k)))
     return b
+
+
+def _mk(xp, device):
+    if xp == "numpy":
+        return (lambda sh: np.zeros(sh, np.float64)), (lambda sh: np.zeros(sh, np.int32))
+    import torch
+    return (lambda sh: torch.zeros(sh, dtype=torch.float64, device=device),
+            lambda sh: torch.zeros(sh, dtype=torch.int32, device=device))
+
+
+def add_car_table(d, xp="numpy", device=None):
+    """Adds the persistent car table (include/pp.h tab_*; empty) to a scene dict."""
+    S = int(d["ego_x"].shape[0])
+    zf, zi = _mk(xp, device)
+    for k in TABLE_FIELDS_I:
+        d[k] = zi((MAX_CARS, S))
+    for k in TABLE_FIELDS_F:
+        d[k] = zf((MAX_CARS, S))
+    return d
+
+
+def alloc_traffic(S, xp="numpy", device=None):
+    zf, zi = _mk(xp, device)
+    return {"n_cars": 0, "lane": zi((MAX_CARS, S)), "seg": zi((MAX_CARS, S)), "t": zf((MAX_CARS, S)),
+            "offset": zf((MAX_CARS, S)), "speed": zf((MAX_CARS, S))}
+
+
+def traffic_struct(t) -> Traffic:
+    T = Traffic()
+    T.n_cars = int(t["n_cars"])
+    for k in ["lane", "seg", "t", "offset", "speed"]:
+        setattr(T, k, _ptr(t[k]))
+    return T
+
+
+def synth_traffic(m, S, seed=0x5EED0001, first=0, device=0, stream=None, car_stride=12):
+    """Rollout start state on the GPU: (scenes with an empty car table, traffic)."""
+    import torch
+    dev = torch.device("cuda", device)
+    d = add_car_table(alloc_scenes(S, car_stride, xp="torch", device=dev), xp="torch", device=dev)
+    t = alloc_traffic(S, xp="torch", device=dev)
+    b, T = scene_struct(d), traffic_struct(t)
+    _check(lib.pp_synth_traffic(m.handle, seed, first, C.byref(b), C.byref(T), device, stream), "pp_synth_traffic")
+    t["n_cars"] = T.n_cars
+    return d, t
+
+
+def synth_traffic_host(m, S, seed=0x5EED0001, first=0, car_stride=12):
+    d = add_car_table(alloc_scenes(S, car_stride))
+    t = alloc_traffic(S)
+    b, T = scene_struct(d), traffic_struct(t)
+    _check(lib.pp_synth_traffic_host(m.handle, seed, first, C.byref(b), C.byref(T)), "pp_synth_traffic_host")
+    t["n_cars"] = T.n_cars
+    return d, t
+
+
+def alloc_log(F, S, N=50, xp="numpy", device=None, plans=True):
+    if xp == "numpy":
+        mk = lambda sh, dt: np.zeros(sh, dt)
+    else:
+        import torch
+        tdt = {"f8": torch.float64, "i4": torch.int32, "u4": torch.int32}
+        mk = lambda sh, dt: torch.zeros(sh, dtype=tdt[dt], device=device)
+    lg = {k: mk((F, S), dt) for k, dt in LOG_FIELDS}
+    if plans:
+        lg["plan_x"] = mk((F, N, S), "f8")
+        lg["plan_y"] = mk((F, N, S), "f8")
+    return lg
+
+
+def log_struct(lg) -> RolloutLog:
+    L = RolloutLog()
+    for k, _ in LOG_FIELDS:
+        setattr(L, k, _ptr(lg.get(k)))
+    L.plan_x, L.plan_y = _ptr(lg.get("plan_x")), _ptr(lg.get("plan_y"))
+    return L
+
+
+def rollout(m, scenes, traffic, prm, result, n_frames, consume=3, sensor_range=300.0, log=None,
+            device=0, stream=None):
+    """pp_rollout: n_frames closed-loop frames on the GPU; scenes/traffic/result updated in place."""
+    b, T, R = scene_struct(scenes), traffic_struct(traffic), result_struct(result)
+    cfg = RolloutCfg(n_frames, consume, float(sensor_range))
+    L = log_struct(log) if log is not None else None
+    _check(lib.pp_rollout(m.handle, C.byref(b), C.byref(T), C.byref(prm), C.byref(cfg), C.byref(R),
+                          C.byref(L) if L is not None else None, device, stream), "pp_rollout")
+
+
+def plan_reset(m, device=0):
+    _check(lib.pp_plan_reset(m.handle, device), "pp_plan_reset")
 
 
 def scenes_to_numpy(d):

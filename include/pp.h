@@ -91,6 +91,20 @@ typedef struct pp_scene_batch {
     const double*  car_y;
     const double*  car_vx;
     const double*  car_vy;
+    /* Optional persistent car table: the reference's cross-frame `std::map<int, Car>
+     * sensor_fusion_cars` (src/main.cpp:1194, 1325-1350). NULL tab_valid = a fresh table every
+     * frame. Otherwise slot [id * n_scenes + s] (id < PP_MAX_CARS; the frame's car ids must be
+     * ascending and < PP_MAX_CARS) holds the car's last matched state: a reported car is
+     * re-matched and its slot overwritten, or erased (valid = 0) when matching fails (:1336-1340);
+     * a car absent from this frame's list keeps its stale slot, which the planner still uses. */
+    int32_t* tab_valid;
+    int32_t* tab_lane;
+    double*  tab_s;
+    double*  tab_d;
+    double*  tab_vs;
+    double*  tab_vd;
+    double*  tab_vx;
+    double*  tab_vy;
 } pp_scene_batch;
 
 /* ---- parameters ---------------------------------------------------------------------------- */
@@ -182,7 +196,8 @@ int32_t pp_eval(pp_map* m, const pp_scene_batch* in, const pp_params* prm, pp_re
 
 /* One telemetry frame, host memory in/out: the onMessage replacement (C = 1, reference decision).
  * prev_x/prev_y hold n_prev points (only the first 10 are read when n_prev >= 10); the car arrays
- * hold n_cars rows in any order (sorted by id internally, as std::map does).
+ * hold n_cars rows in any order (sorted by id internally, as std::map does). The car table
+ * persists across calls like the reference's (see pp_plan_reset) when every id is < PP_MAX_CARS.
  * *target_lane is read (cross-frame state) and updated. Writes up to 50 points. */
 int32_t pp_plan_frame(pp_map* m, int32_t device,
                       double ego_x, double ego_y, double ego_yaw_deg, double ego_speed_mph,
@@ -199,6 +214,64 @@ int32_t pp_synth_scenes(pp_map* m, uint64_t seed, int64_t first_scene, pp_scene_
 /* The same generator on the host (identical bits except ego_yaw_deg, which goes through atan2). */
 int32_t pp_synth_scenes_host(const pp_map* m, uint64_t seed, int64_t first_scene,
                              pp_scene_batch* out);
+
+/* ---- closed-loop rollout ------------------------------------------- */
+/* A simulator shim closes the loop around the planner: per frame, pp_eval plans every scene, then
+ * the simulator drives `consume` points of each plan (the ego ends on point consume-1; speed and
+ * yaw from the last two driven points; previous_path = the undriven rest), sets the cross-frame
+ * target lane (src/main.cpp:1195) to the plan's lane (winner / n_speeds), advances the traffic by
+ * consume * 0.02 s and reports the cars within sensor_range (ascending id) as the next frame's
+ * sensor_fusion; the others become stale car-table entries (tab_* above, required). */
+typedef struct pp_traffic {        /* device SoA [j * n_scenes + s]; car j has id j               */
+    int32_t  n_cars;               /* cars per scene (<= PP_MAX_CARS)                               */
+    int32_t  _pad;
+    int32_t* lane;                 /* lane-centre polyline it follows                              */
+    int32_t* seg;                  /* segment (ends at waypoint seg) and fraction t on it          */
+    double*  t;
+    double*  offset;               /* lateral offset from the lane centre (right-hand normal)      */
+    double*  speed;                /* m/s along the lane                                           */
+} pp_traffic;
+
+typedef struct pp_rollout_cfg {
+    int32_t n_frames;
+    int32_t consume;               /* points the simulator drives per frame (>= 1)                 */
+    double  sensor_range;          /* metres; cars farther from the ego are not reported           */
+} pp_rollout_cfg;
+
+/* Optional per-frame records, [f * n_scenes + s] (plans: [(f * n_points + i) * n_scenes + s]);
+ * any pointer may be NULL. The ego fields are the telemetry the frame was planned from. */
+typedef struct pp_rollout_log {
+    double*   ego_x;
+    double*   ego_y;
+    double*   ego_speed_mph;
+    int32_t*  target_lane;        /* after the frame (the plan's lane)                             */
+    int32_t*  winner;
+    int32_t*  n_out;
+    uint32_t* status;
+    int32_t*  n_cars;             /* sensor_fusion rows the frame was planned from                 */
+    double*   plan_x;
+    double*   plan_y;
+} pp_rollout_log;
+
+/* Runs cfg->n_frames frames; `telemetry` (with its car table), `traffic` and `result` (per-frame
+ * plan buffers, pp_eval layout) are device state updated in place, so consecutive calls continue
+ * the episode. n_draws must be <= 1 and emit_paths 0. */
+int32_t pp_rollout(pp_map* m, pp_scene_batch* telemetry, pp_traffic* traffic,
+                   const pp_params* prm, const pp_rollout_cfg* cfg, pp_result* result,
+                   pp_rollout_log* log, int32_t device, void* hip_stream);
+
+/* Rollout start state: writes the synthetic scenes of pp_synth_scenes (same seed and indices)
+ * into `telemetry` and their traffic into `out` (n_cars = 12): car j starts exactly where the
+ * scene reports it, on its lane with its lateral offset and speed. Empties the car table of
+ * `telemetry` when its tab_valid is set. */
+int32_t pp_synth_traffic(pp_map* m, uint64_t seed, int64_t first_scene, pp_scene_batch* telemetry,
+                         pp_traffic* out, int32_t device, void* hip_stream);
+int32_t pp_synth_traffic_host(const pp_map* m, uint64_t seed, int64_t first_scene,
+                              pp_scene_batch* telemetry, pp_traffic* out);
+
+/* pp_plan_frame keeps the reference's car table across calls (per map and device, cars with ids
+ * in [0, PP_MAX_CARS)); pp_plan_reset empties it (a new episode). */
+int32_t pp_plan_reset(pp_map* m, int32_t device);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
  * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the

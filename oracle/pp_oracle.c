@@ -588,29 +588,55 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
     int nc = 0;
     int ncar = in->n_cars[s];
     if (ncar > in->car_stride) ncar = in->car_stride;
-    for (int j = 0; j < ncar; j++) {
+    /* with a car table (the reference's persistent std::map, :1194): ids 0..PP_MAX_CARS-1 in
+     * order, each reported this frame (re-matched: slot overwritten, or erased, :1329-1348) or
+     * taken from its stale slot; without one: the frame's rows in (ascending id) order */
+    const int tab = in->tab_valid != NULL;
+    const int iters = tab ? PP_MAX_CARS : ncar;
+    int p = 0;
+    for (int it = 0; it < iters; it++) {
+        int row = it;
+        if (tab) {
+            while (p < ncar && in->car_id[(int64_t)p * S + s] < it) p++;
+            row = (p < ncar && in->car_id[(int64_t)p * S + s] == it) ? p++ : -1;
+        }
+        const int64_t tix = (int64_t)it * S + s;
         OCar c;
         memset(&c, 0, sizeof(c));
-        int64_t ix = (int64_t)j * S + s;
-        c.id = in->car_id[ix];
-        c.x = in->car_x[ix];
-        c.y = in->car_y[ix];
-        c.vx = in->car_vx[ix];
-        c.vy = in->car_vy[ix];
-        if (draw > 0) {
-            const uint64_t gs = (uint64_t)(P->noise_first_scene + s);
-            c.x += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, j, 0);
-            c.y += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, j, 1);
-            c.vx += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, j, 2);
-            c.vy += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, j, 3);
+        if (row >= 0) {
+            int64_t ix = (int64_t)row * S + s;
+            c.id = in->car_id[ix];
+            c.x = in->car_x[ix];
+            c.y = in->car_y[ix];
+            c.vx = in->car_vx[ix];
+            c.vy = in->car_vy[ix];
+            if (draw > 0) {
+                const uint64_t gs = (uint64_t)(P->noise_first_scene + s);
+                c.x += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, row, 0);
+                c.y += P->noise_pos_sigma * mc_gauss(P->noise_seed, gs, draw, row, 1);
+                c.vx += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, row, 2);
+                c.vy += P->noise_vel_sigma * mc_gauss(P->noise_seed, gs, draw, row, 3);
+            }
+            int nwp = 0;
+            if (!lane_matching(m, &pr->fr, c.x, c.y, &c.s, &c.d, &c.lane, &nwp)) {
+                pr->status |= PP_ST_CAR_UNMATCHED;
+                if (tab) in->tab_valid[tix] = 0;
+                continue;
+            }
+            P2 v = {c.vx, c.vy};
+            project_speed(m, v, nwp, &c.vs, &c.vd);
+            if (tab) {
+                in->tab_valid[tix] = 1; in->tab_lane[tix] = c.lane;
+                in->tab_s[tix] = c.s; in->tab_d[tix] = c.d; in->tab_vs[tix] = c.vs; in->tab_vd[tix] = c.vd;
+                in->tab_vx[tix] = c.vx; in->tab_vy[tix] = c.vy;
+            }
+        } else {
+            if (!in->tab_valid[tix]) continue;
+            c.id = it;
+            c.lane = in->tab_lane[tix];
+            c.s = in->tab_s[tix]; c.d = in->tab_d[tix]; c.vs = in->tab_vs[tix]; c.vd = in->tab_vd[tix];
+            c.vx = in->tab_vx[tix]; c.vy = in->tab_vy[tix];
         }
-        int nwp = 0;
-        if (!lane_matching(m, &pr->fr, c.x, c.y, &c.s, &c.d, &c.lane, &nwp)) {
-            pr->status |= PP_ST_CAR_UNMATCHED;
-            continue;
-        }
-        P2 v = {c.vx, c.vy};
-        project_speed(m, v, nwp, &c.vs, &c.vd);
         cars[nc++] = c;
     }
     pr->nmatched = nc;
@@ -1012,5 +1038,141 @@ int ppo_struct_sizes(int64_t* out4) {
     out4[1] = sizeof(pp_params);
     out4[2] = sizeof(pp_result);
     out4[3] = sizeof(pp_scene_info);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Closed-loop rollout (include/pp.h pp_rollout): the simulator shim, restated               */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { double *len, *tx, *ty; int n; const OMap* m; } OLanes;   /* [lane * n + i] */
+
+static void olanes_init(OLanes* L, const OMap* m) {
+    const int n = m->n;
+    L->n = n; L->m = m;
+    L->len = (double*)malloc(sizeof(double) * 3 * n);
+    L->tx = (double*)malloc(sizeof(double) * 3 * n);
+    L->ty = (double*)malloc(sizeof(double) * 3 * n);
+    for (int r = 0; r < 3; r++)
+        for (int i = 0; i < n; i++) {
+            const int q = wpi(m, i - 1);
+            const double dx = m->lc[i][r].x - m->lc[q][r].x, dy = m->lc[i][r].y - m->lc[q][r].y;
+            const double len = sqrt(dx * dx + dy * dy);
+            L->len[r * n + i] = len;
+            L->tx[r * n + i] = (m->lc[i][r].x - m->lc[q][r].x) / len;
+            L->ty[r * n + i] = (m->lc[i][r].y - m->lc[q][r].y) / len;
+        }
+}
+
+/* advance (seg, t) by dist >= 0 along the lane polyline (segment i ends at waypoint i) */
+static void o_lane_advance(const OLanes* L, int lane, int* seg, double* t, double dist) {
+    const int n = L->n;
+    int i = *seg;
+    double tt = *t;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        const double len = L->len[lane * n + i];
+        const double rem = (1.0 - tt) * len;
+        if (dist <= rem || it == 4 * n + 7) { tt = tt + dist / len; break; }
+        dist -= rem; tt = 0.0; i = (i + 1 == n) ? 0 : i + 1;
+    }
+    *seg = i;
+    *t = tt;
+}
+
+static void o_traffic_car(const OLanes* L, int lane, int seg, double t, double off, double v,
+                          double* x, double* y, double* vx, double* vy) {
+    const int n = L->n;
+    const int ip = seg == 0 ? n - 1 : seg - 1;
+    const P2 A = L->m->lc[ip][lane], B = L->m->lc[seg][lane];
+    const double px = A.x + (B.x - A.x) * t, py = A.y + (B.y - A.y) * t;
+    const double ux = L->tx[lane * n + seg], uy = L->ty[lane * n + seg];
+    *x = px + uy * off;
+    *y = py - ux * off;
+    *vx = ux * v;
+    *vy = uy * v;
+}
+
+/* in: host batch with a car table, updated in place; res: per-frame plan buffers (pp_eval layout) */
+int ppo_rollout(const double* wx, const double* wy, int n_wp, pp_scene_batch* in, pp_traffic* tr,
+                const pp_params* P, const pp_rollout_cfg* cfg, pp_result* res, pp_rollout_log* log) {
+    if (!in || !tr || !P || !cfg || !res || !in->tab_valid || P->n_draws > 1 || P->emit_paths ||
+        cfg->consume < 1 || tr->n_cars > in->car_stride)
+        return -1;
+    OMap m;
+    if (n_wp < 2 || omap_init(&m, wx, wy, n_wp)) return -1;
+    OLanes L;
+    olanes_init(&L, &m);
+    const int64_t S = in->n_scenes;
+    const int N = P->n_points;
+    const double range2 = cfg->sensor_range * cfg->sensor_range;
+    double* ex = (double*)in->ego_x;
+    double* ey = (double*)in->ego_y;
+    double* eyaw = (double*)in->ego_yaw_deg;
+    double* espd = (double*)in->ego_speed_mph;
+    double* px = (double*)in->prev_x;
+    double* py = (double*)in->prev_y;
+    for (int f = 0; f < cfg->n_frames; f++) {
+        if (ppo_eval_range(wx, wy, n_wp, in, P, res, 0, S)) { free(L.len); free(L.tx); free(L.ty); omap_free(&m); return -1; }
+        for (int64_t s = 0; s < S; s++) {
+            const int n_out = res->n_out[s];
+            const int T = res->winner[s] / P->n_speeds;
+            const double x0 = ex[s], y0 = ey[s];
+            const int64_t fs = (int64_t)f * S + s;
+            if (log) {
+                if (log->ego_x) log->ego_x[fs] = x0;
+                if (log->ego_y) log->ego_y[fs] = y0;
+                if (log->ego_speed_mph) log->ego_speed_mph[fs] = espd[s];
+                if (log->target_lane) log->target_lane[fs] = T;
+                if (log->winner) log->winner[fs] = res->winner[s];
+                if (log->n_out) log->n_out[fs] = n_out;
+                if (log->status) log->status[fs] = res->status[s];
+                if (log->n_cars) log->n_cars[fs] = in->n_cars[s];
+                if (log->plan_x)
+                    for (int i = 0; i < N; i++) {
+                        log->plan_x[((int64_t)f * N + i) * S + s] = res->next_x[(int64_t)i * S + s];
+                        log->plan_y[((int64_t)f * N + i) * S + s] = res->next_y[(int64_t)i * S + s];
+                    }
+            }
+            const int kk = n_out < cfg->consume ? n_out : cfg->consume;
+            double nx = x0, ny = y0, qx = x0, qy = y0;
+            if (kk >= 1) { nx = res->next_x[(int64_t)(kk - 1) * S + s]; ny = res->next_y[(int64_t)(kk - 1) * S + s]; }
+            if (kk >= 2) { qx = res->next_x[(int64_t)(kk - 2) * S + s]; qy = res->next_y[(int64_t)(kk - 2) * S + s]; }
+            const double dx = nx - qx, dy = ny - qy;
+            const double dist = sqrt(dx * dx + dy * dy);
+            ex[s] = nx; ey[s] = ny;
+            espd[s] = dist * 50 * 2.237;
+            if (dist > 0) eyaw[s] = atan2(dy, dx) * 180.0 / O_PI;
+            const int np = n_out - kk;
+            for (int i = 0; i < PP_PREV_KEEP; i++) {
+                const int ok = i < np;
+                px[(int64_t)i * S + s] = ok ? res->next_x[(int64_t)(kk + i) * S + s] : 0.0;
+                py[(int64_t)i * S + s] = ok ? res->next_y[(int64_t)(kk + i) * S + s] : 0.0;
+            }
+            ((int32_t*)in->n_prev)[s] = np;
+            ((int32_t*)in->prev_target_lane)[s] = T;
+            int nc = 0;
+            for (int j = 0; j < tr->n_cars; j++) {
+                const int64_t tx = (int64_t)j * S + s;
+                const int lane = tr->lane[tx];
+                int seg = tr->seg[tx];
+                double t = tr->t[tx];
+                const double v = tr->speed[tx];
+                o_lane_advance(&L, lane, &seg, &t, v * 0.02 * cfg->consume);
+                tr->seg[tx] = seg; tr->t[tx] = t;
+                double cx, cy, cvx, cvy;
+                o_traffic_car(&L, lane, seg, t, tr->offset[tx], v, &cx, &cy, &cvx, &cvy);
+                const double rx = cx - nx, ry = cy - ny;
+                if (rx * rx + ry * ry <= range2 && nc < in->car_stride) {
+                    const int64_t ix = (int64_t)nc * S + s;
+                    ((int32_t*)in->car_id)[ix] = j;
+                    ((double*)in->car_x)[ix] = cx; ((double*)in->car_y)[ix] = cy;
+                    ((double*)in->car_vx)[ix] = cvx; ((double*)in->car_vy)[ix] = cvy;
+                    nc++;
+                }
+            }
+            ((int32_t*)in->n_cars)[s] = nc;
+        }
+    }
+    free(L.len); free(L.tx); free(L.ty);
+    omap_free(&m);
     return 0;
 }

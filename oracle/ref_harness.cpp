@@ -178,3 +178,179 @@ extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_s
     }
     return 0;
 }
+
+// ---- closed-loop rollout (include/pp.h pp_rollout semantics) --------------------------------
+// The reference frame (src/main.cpp:1233-1457) with the lambda's cross-frame state kept per
+// scene exactly as main() keeps it: the std::map<int, Car> sensor_fusion_cars (:1194, stale
+// entries included) and target_lane (:1195). The simulator shim around it is ours (restated
+// from include/pp.h: drive `consume` points, lane-following traffic, sensor range).
+namespace refh {
+
+static void rollout_frame(Map& map, std::map<int, Car>& sensor_fusion_cars, const pp_scene_batch* in,
+                          int64_t s, int& target_lane, vector<Point>& out) {
+    const int64_t S = in->n_scenes;
+    double ego_x = in->ego_x[s];
+    double ego_y = in->ego_y[s];
+    double ego_yaw = in->ego_yaw_deg[s];
+    double ego_speed = in->ego_speed_mph[s];
+    ego_speed /= 2.237;
+    double ego_acc = 0;
+    vector<Point> prev_trajectory;
+    double delta_t0 = 0;
+    Point ego_speed_vector;
+    int prev_trajectory_length = 10;
+    if (in->n_prev[s] >= prev_trajectory_length) {                       // :1261-1282
+        for (int i = 0; i < prev_trajectory_length; i++)
+            prev_trajectory.push_back(Point(in->prev_x[i * S + s], in->prev_y[i * S + s]));
+        double v2 = (prev_trajectory[prev_trajectory_length - 2] - prev_trajectory[prev_trajectory_length - 3]).length();
+        ego_speed_vector = prev_trajectory[prev_trajectory_length - 1] - prev_trajectory[prev_trajectory_length - 2];
+        double v3 = ego_speed_vector.length();
+        ego_acc = (v3 - v2) * 50;
+        ego_speed = v3 * 50;
+        ego_speed_vector.x *= 50;
+        ego_speed_vector.y *= 50;
+        ego_x = prev_trajectory[prev_trajectory_length - 1].x;
+        ego_y = prev_trajectory[prev_trajectory_length - 1].y;
+        delta_t0 = prev_trajectory_length / 50.0;
+    }
+    map.init_reference_waypoint(ego_x, ego_y);                           // :1299
+    int ego_lane;
+    double ego_s, ego_d;
+    if (!map.lane_matching(ego_x, ego_y, ego_s, ego_d, ego_lane)) {
+        ego_s = ego_d = 0;
+        ego_lane = 0;
+    }
+    double ego_vs, ego_vd;
+    map.project_speed(ego_speed_vector, map.reference_waypoint_id, &ego_vs, &ego_vd);
+    if (ego_acc > maximum_acc) ego_acc = maximum_acc;
+    if (ego_acc < -maximum_acc) ego_acc = -maximum_acc;
+    int ncar = in->n_cars[s] < in->car_stride ? in->n_cars[s] : in->car_stride;
+    for (int j = 0; j < ncar; j++) {                                     // :1325-1350
+        int id = in->car_id[j * S + s];
+        auto& car = sensor_fusion_cars[id];
+        car.id = id;
+        car.x = in->car_x[j * S + s];
+        car.y = in->car_y[j * S + s];
+        car.vx = in->car_vx[j * S + s];
+        car.vy = in->car_vy[j * S + s];
+        int next_wp_id = 0;
+        if (!map.lane_matching(car.x, car.y, car.s, car.d, car.lane, &next_wp_id))
+            sensor_fusion_cars.erase(sensor_fusion_cars.find(id));
+        else
+            map.project_speed(Point(car.vx, car.vy), next_wp_id, &car.vs, &car.vd);
+    }
+    LaneChangePlanner lane_change_planner;                               // :1352-1356
+    target_lane = lane_change_planner.calculate_target_lane(sensor_fusion_cars, ego_lane, target_lane,
+                                                            ego_s, ego_vs, delta_t0);
+    if (target_lane != ego_lane) {                                       // :1358-1369
+        double d_of_target_lane = map.get_lane_center_offset(target_lane);
+        double lane_d_diff = fabs(ego_vd * 1.0 + ego_d - d_of_target_lane);
+        if (lane_d_diff > 6.0) target_lane = ego_lane;
+    }
+    int in_id, t_id;                                                     // :1383-1438
+    double in_s, t_s;
+    select_follow(sensor_fusion_cars, delta_t0, ego_s, ego_d, map.get_lane_center_offset(target_lane),
+                  in_id, in_s, t_id, t_s);
+    SpeedController speed_controller(ego_speed);
+    apply_limits(sensor_fusion_cars, speed_controller, in_id, in_s, t_id, t_s, ego_s, ego_speed, ego_acc);
+    TrajectoryBuilder trajectory;                                        // :1448
+    out = trajectory.build(prev_trajectory, ego_x, ego_y, ego_yaw, ego_lane, target_lane, ego_d, ego_vd,
+                           map, speed_controller);
+}
+
+}  // namespace refh
+
+// in: host telemetry batch (updated in place; its tab_* are not used: the std::map is the table)
+extern "C" int ref_rollout(const double* wx, const double* wy, int n_wp, pp_scene_batch* in,
+                           pp_traffic* tr, const pp_rollout_cfg* cfg, pp_rollout_log* log) {
+    Map map;
+    vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
+    map.Init(X, Y);
+    const int n = (int)map.waypoints.size();
+    vector<double> len(3 * n), tx(3 * n), ty(3 * n);
+    for (int r = 0; r < 3; r++)
+        for (int i = 0; i < n; i++) {
+            const int q = (i - 1 + n) % n;
+            const Point a = map.waypoints[q].lane_center[r], b = map.waypoints[i].lane_center[r];
+            const double dx = b.x - a.x, dy = b.y - a.y;
+            len[r * n + i] = sqrt(dx * dx + dy * dy);
+            tx[r * n + i] = (b.x - a.x) / len[r * n + i];
+            ty[r * n + i] = (b.y - a.y) / len[r * n + i];
+        }
+    const int64_t S = in->n_scenes;
+    const int N = 50;
+    const double range2 = cfg->sensor_range * cfg->sensor_range;
+    vector<std::map<int, Car>> tables(S);
+    double* ex = (double*)in->ego_x;
+    double* ey = (double*)in->ego_y;
+    double* eyaw = (double*)in->ego_yaw_deg;
+    double* espd = (double*)in->ego_speed_mph;
+    for (int f = 0; f < cfg->n_frames; f++) {
+        for (int64_t s = 0; s < S; s++) {
+            int target_lane = in->prev_target_lane[s];
+            vector<Point> P;
+            refh::rollout_frame(map, tables[s], in, s, target_lane, P);
+            const int n_out = (int)P.size();
+            const int64_t fs = (int64_t)f * S + s;
+            if (log->ego_x) log->ego_x[fs] = ex[s];
+            if (log->ego_y) log->ego_y[fs] = ey[s];
+            if (log->ego_speed_mph) log->ego_speed_mph[fs] = espd[s];
+            if (log->target_lane) log->target_lane[fs] = target_lane;
+            if (log->n_out) log->n_out[fs] = n_out;
+            if (log->n_cars) log->n_cars[fs] = in->n_cars[s];
+            if (log->plan_x)
+                for (int i = 0; i < N; i++) {
+                    log->plan_x[((int64_t)f * N + i) * S + s] = i < n_out ? P[i].x : 0.0;
+                    log->plan_y[((int64_t)f * N + i) * S + s] = i < n_out ? P[i].y : 0.0;
+                }
+            // simulator shim
+            const int kk = n_out < cfg->consume ? n_out : cfg->consume;
+            double nx = ex[s], ny = ey[s], qx = ex[s], qy = ey[s];
+            if (kk >= 1) { nx = P[kk - 1].x; ny = P[kk - 1].y; }
+            if (kk >= 2) { qx = P[kk - 2].x; qy = P[kk - 2].y; }
+            const double dx = nx - qx, dy = ny - qy;
+            const double dist = sqrt(dx * dx + dy * dy);
+            ex[s] = nx; ey[s] = ny;
+            espd[s] = dist * 50 * 2.237;
+            if (dist > 0) eyaw[s] = atan2(dy, dx) * 180.0 / 3.14159265358979323846;
+            const int np = n_out - kk;
+            for (int i = 0; i < PP_PREV_KEEP; i++) {
+                ((double*)in->prev_x)[i * S + s] = i < np ? P[kk + i].x : 0.0;
+                ((double*)in->prev_y)[i * S + s] = i < np ? P[kk + i].y : 0.0;
+            }
+            ((int32_t*)in->n_prev)[s] = np;
+            ((int32_t*)in->prev_target_lane)[s] = target_lane;
+            int nc = 0;
+            for (int j = 0; j < tr->n_cars; j++) {
+                const int64_t k = (int64_t)j * S + s;
+                const int lane = tr->lane[k];
+                int seg = tr->seg[k];
+                double t = tr->t[k];
+                const double v = tr->speed[k];
+                double dd = v * 0.02 * cfg->consume;
+                for (int it = 0; it < 4 * n + 8; it++) {
+                    const double L = len[lane * n + seg];
+                    const double rem = (1.0 - t) * L;
+                    if (dd <= rem || it == 4 * n + 7) { t = t + dd / L; break; }
+                    dd -= rem; t = 0.0; seg = (seg + 1 == n) ? 0 : seg + 1;
+                }
+                tr->seg[k] = seg; tr->t[k] = t;
+                const int ip = seg == 0 ? n - 1 : seg - 1;
+                const Point a = map.waypoints[ip].lane_center[lane], b = map.waypoints[seg].lane_center[lane];
+                const double px = a.x + (b.x - a.x) * t, py = a.y + (b.y - a.y) * t;
+                const double ux = tx[lane * n + seg], uy = ty[lane * n + seg];
+                const double cx = px + uy * tr->offset[k], cy = py - ux * tr->offset[k];
+                const double rx = cx - nx, ry = cy - ny;
+                if (rx * rx + ry * ry <= range2 && nc < in->car_stride) {
+                    const int64_t ix = (int64_t)nc * S + s;
+                    ((int32_t*)in->car_id)[ix] = j;
+                    ((double*)in->car_x)[ix] = cx; ((double*)in->car_y)[ix] = cy;
+                    ((double*)in->car_vx)[ix] = ux * v; ((double*)in->car_vy)[ix] = uy * v;
+                    nc++;
+                }
+            }
+            ((int32_t*)in->n_cars)[s] = nc;
+        }
+    }
+    return 0;
+}

@@ -39,6 +39,10 @@ def load_oracle():
     lib.ppo_struct_sizes.argtypes = [C.POINTER(C.c_int64)]
     lib.ppo_mc_gauss.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int]
     lib.ppo_mc_gauss.restype = C.c_double
+    lib.ppo_rollout.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.POINTER(ppamd.Traffic),
+                                C.POINTER(ppamd.Params), C.POINTER(ppamd.RolloutCfg), C.POINTER(ppamd.Result),
+                                C.POINTER(ppamd.RolloutLog)]
+    lib.ppo_rollout.restype = C.c_int
     return lib
 
 
@@ -80,7 +84,47 @@ def load_ref():
     lib.ref_eval.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.c_int, _dp, C.c_int, _dp,
                              C.POINTER(C.c_int), C.POINTER(C.c_int), _dp, C.POINTER(C.c_int), _dp]
     lib.ref_eval.restype = C.c_int
+    lib.ref_rollout.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.POINTER(ppamd.Traffic),
+                                C.POINTER(ppamd.RolloutCfg), C.POINTER(ppamd.RolloutLog)]
+    lib.ref_rollout.restype = C.c_int
     return lib
+
+
+def copy_state(scenes, traffic):
+    return ({k: np.array(v, copy=True) for k, v in scenes.items()},
+            {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in traffic.items()})
+
+
+def oracle_rollout(lib, wx, wy, scenes, traffic, prm, n_frames, consume=3, sensor_range=300.0,
+                   plans=True):
+    """C restatement closed loop; scenes/traffic (host, with car table) are updated in place."""
+    S = int(scenes["ego_x"].shape[0])
+    lg = ppamd.alloc_log(n_frames, S, prm.n_points, plans=plans)
+    res = ppamd.alloc_result(S, prm)
+    b, T, R, L = (ppamd.scene_struct(scenes), ppamd.traffic_struct(traffic), ppamd.result_struct(res),
+                  ppamd.log_struct(lg))
+    cfg = ppamd.RolloutCfg(n_frames, consume, float(sensor_range))
+    wx = np.ascontiguousarray(wx, np.float64)
+    wy = np.ascontiguousarray(wy, np.float64)
+    rc = lib.ppo_rollout(wx.ctypes.data_as(_dp), wy.ctypes.data_as(_dp), len(wx), C.byref(b), C.byref(T),
+                         C.byref(prm), C.byref(cfg), C.byref(R), C.byref(L))
+    assert rc == 0, rc
+    return lg
+
+
+def ref_rollout(lib, wx, wy, scenes, traffic, n_frames, consume=3, sensor_range=300.0, plans=True):
+    """The reference's own frame code (persistent std::map car table) in the same closed loop."""
+    S = int(scenes["ego_x"].shape[0])
+    lg = ppamd.alloc_log(n_frames, S, 50, plans=plans)
+    b, T, L = ppamd.scene_struct(scenes), ppamd.traffic_struct(traffic), ppamd.log_struct(lg)
+    cfg = ppamd.RolloutCfg(n_frames, consume, float(sensor_range))
+    wx = np.ascontiguousarray(wx, np.float64)
+    wy = np.ascontiguousarray(wy, np.float64)
+    with quiet_stdout():
+        rc = lib.ref_rollout(wx.ctypes.data_as(_dp), wy.ctypes.data_as(_dp), len(wx), C.byref(b), C.byref(T),
+                             C.byref(cfg), C.byref(L))
+    assert rc == 0, rc
+    return lg
 
 
 def highway_map():
@@ -118,19 +162,27 @@ def ref_eval(lib, wx, wy, scenes, n_speeds, speed_offsets, with_frame=True):
     wy = np.ascontiguousarray(wy, np.float64)
     ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
     dp = lambda a: a.ctypes.data_as(_dp)
-    # the reference prints warnings to stdout ("spline input error" ...): silence fd 1
-    sys.stdout.flush()
-    saved = os.dup(1)
-    devnull = os.open(os.devnull, os.O_WRONLY)
-    os.dup2(devnull, 1)
-    try:
+    with quiet_stdout():
         rc = lib.ref_eval(dp(wx), dp(wy), len(wx), C.byref(b), n_speeds, dp(offs), int(with_frame),
                           dp(out["ref_next"]), ip(out["ref_n"]), ip(out["ref_T"]),
                           dp(out["paths"]), ip(out["path_len"]), dp(out["info"]))
-    finally:
-        C.CDLL(None).fflush(None)      # drain the reference's printf buffer into /dev/null
-        os.dup2(saved, 1)
-        os.close(saved)
-        os.close(devnull)
     assert rc == 0
     return out
+
+
+class quiet_stdout:
+    """The reference prints warnings to stdout ("spline input error", "detected collision"):
+    silence fd 1 around a call into it."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        self.devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(self.devnull, 1)
+
+    def __exit__(self, *a):
+        C.CDLL(None).fflush(None)      # drain the reference's printf buffer into /dev/null
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        os.close(self.devnull)
+        return False

@@ -1,0 +1,157 @@
+"""Closed-loop rollout: the planner's cross-frame state — the reference's
+persistent std::map car table with stale entries (src/main.cpp:1194, 1325-1350) and target_lane
+(:1195) — driven by the simulator shim of include/pp.h (pp_rollout).
+
+Pinning: tests/golden/rollout_golden.npz holds 600-frame replays made by the reference's own frame
+code (tests/golden/make_rollout_golden.py); the C restatement must reproduce them bit for bit; the
+HIP rollout must match them within 1e-6 m, and match the restatement frame by frame."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import ppamd
+
+TOL = 1e-6
+G = np.load(oracle_lib.GOLDEN + "/rollout_golden.npz")
+VARIANTS = ["r120", "rinf"]
+LOG_KEYS = ["ego_x", "ego_y", "ego_speed_mph", "target_lane", "n_out", "n_cars"]
+
+
+def golden_state(v):
+    sc = {k[len(v) + 7:]: np.array(G[k]) for k in G.files if k.startswith(f"{v}_scene_")}
+    tr = {k[len(v) + 9:]: np.array(G[k]) for k in G.files if k.startswith(f"{v}_traffic_")}
+    tr["n_cars"] = int(tr["n_cars"])
+    return sc, tr
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    wx, wy = oracle_lib.highway_map()
+    return {"m": ppamd.Map(wx, wy), "wx": wx, "wy": wy, "olib": oracle_lib.load_oracle(),
+            "rlib": oracle_lib.load_ref()}
+
+
+@pytest.mark.parametrize("v", VARIANTS)
+def test_restatement_reproduces_reference_replay(cpu, v):
+    sc, tr = golden_state(v)
+    F = int(G["frames"])
+    lg = oracle_lib.oracle_rollout(cpu["olib"], cpu["wx"], cpu["wy"], sc, tr, ppamd.default_params(n_speeds=1),
+                                   F, int(G["consume"]), float(G[f"{v}_range"]))
+    for k in LOG_KEYS:
+        np.testing.assert_array_equal(lg[k], G[f"{v}_ref_{k}"], err_msg=k)
+    pf = int(G["plan_frames"])
+    np.testing.assert_array_equal(lg["plan_x"][:pf], G[f"{v}_ref_plan_x"])
+    np.testing.assert_array_equal(lg["plan_y"][:pf], G[f"{v}_ref_plan_y"])
+    if v == "r120":
+        # cars leave the sensor range: the table keeps stale entries the planner still uses
+        assert (sc["tab_valid"].sum(0) > sc["n_cars"]).any()
+
+
+def test_start_state_matches_synthetic_scenes(cpu):
+    """pp_synth_traffic_host writes the same scenes as pp_synth_scenes_host, and every car's
+    traffic state reproduces its reported position."""
+    sc, tr = ppamd.synth_traffic_host(cpu["m"], 64, seed=99)
+    ref = ppamd.synth_host(cpu["m"], 64, seed=99)
+    for k in ref:
+        np.testing.assert_array_equal(sc[k], ref[k], err_msg=k)
+    assert tr["n_cars"] == 12 and not sc["tab_valid"].any()
+
+
+@pytest.mark.skipif(oracle_lib.load_ref() is None, reason="oracle/_ref not built (no reference here)")
+@pytest.mark.parametrize("seed,consume,rng", [(3, 1, 80.0), (4, 5, 200.0), (5, 3, 60.0)])
+def test_restatement_vs_reference_live(cpu, seed, consume, rng):
+    """Fresh seeds, other consume counts and ranges, against the reference build itself."""
+    sc, tr = ppamd.synth_traffic_host(cpu["m"], 6, seed=seed)
+    a, b = oracle_lib.copy_state(sc, tr), oracle_lib.copy_state(sc, tr)
+    lo = oracle_lib.oracle_rollout(cpu["olib"], cpu["wx"], cpu["wy"], *a, ppamd.default_params(n_speeds=1),
+                                   300, consume, rng)
+    lr = oracle_lib.ref_rollout(cpu["rlib"], cpu["wx"], cpu["wy"], *b, 300, consume, rng)
+    for k in LOG_KEYS + ["plan_x", "plan_y"]:
+        np.testing.assert_array_equal(lo[k], lr[k], err_msg=k)
+
+
+@pytest.mark.gpu
+class TestRolloutGPU:
+    @pytest.fixture(scope="class")
+    def env(self):
+        import torch
+        wx, wy = oracle_lib.highway_map()
+        return {"torch": torch, "m": ppamd.Map(wx, wy), "wx": wx, "wy": wy,
+                "olib": oracle_lib.load_oracle(), "dev": torch.device("cuda", 0)}
+
+    def upload(self, env, sc, tr):
+        t = env["torch"]
+        d = {k: t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
+        g = {k: (t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) if isinstance(v, np.ndarray) else v)
+             for k, v in tr.items()}
+        return d, g
+
+    @pytest.mark.parametrize("v", VARIANTS)
+    def test_gpu_replay_matches_reference(self, env, v):
+        sc, tr = golden_state(v)
+        d, g = self.upload(env, sc, tr)
+        F, S = int(G["frames"]), sc["ego_x"].shape[0]
+        prm = ppamd.default_params(n_speeds=1)
+        res = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
+        lg = ppamd.alloc_log(F, S, 50, xp="torch", device=env["dev"])
+        ppamd.rollout(env["m"], d, g, prm, res, F, int(G["consume"]), float(G[f"{v}_range"]), lg)
+        env["torch"].cuda.synchronize()
+        got = {k: x.cpu().numpy() for k, x in lg.items()}
+        for k in ["target_lane", "n_out", "n_cars"]:
+            np.testing.assert_array_equal(got[k], G[f"{v}_ref_{k}"], err_msg=k)
+        for k in ["ego_x", "ego_y"]:
+            e = np.abs(got[k] - G[f"{v}_ref_{k}"]).max()
+            assert e <= TOL, (k, e)
+        pf = int(G["plan_frames"])
+        for k in ["plan_x", "plan_y"]:
+            e = np.abs(got[k][:pf] - G[f"{v}_ref_{k}"]).max()
+            assert e <= TOL, (k, e)
+        print(f"{v}: {S} scenes x {F} frames, max |d ego| "
+              f"{max(np.abs(got['ego_x'] - G[f'{v}_ref_ego_x']).max(), np.abs(got['ego_y'] - G[f'{v}_ref_ego_y']).max()):.2e} m")
+
+    def test_frame_by_frame_vs_restatement(self, env):
+        """Every frame of a GPU episode, re-run by the restatement from the GPU's own state:
+        plan within 1e-6 m, the car table and traffic identical, the next telemetry identical
+        (yaw within 1e-9 deg: the simulator's atan2 is the device library's)."""
+        t = env["torch"]
+        S, F = 384, 40
+        d, g = ppamd.synth_traffic(env["m"], S, seed=11, device=0)
+        prm = ppamd.default_params(n_speeds=1)
+        res = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
+        for f in range(F):
+            sc = {k: x.cpu().numpy() for k, x in d.items()}
+            tr = {k: (x.cpu().numpy() if isinstance(x, t.Tensor) else x) for k, x in g.items()}
+            lo = oracle_lib.oracle_rollout(env["olib"], env["wx"], env["wy"], sc, tr, prm, 1, 3, 100.0)
+            lg = ppamd.alloc_log(1, S, 50, xp="torch", device=env["dev"])
+            ppamd.rollout(env["m"], d, g, prm, res, 1, 3, 100.0, lg)
+            t.cuda.synchronize()
+            got = {k: x.cpu().numpy() for k, x in lg.items()}
+            np.testing.assert_array_equal(got["target_lane"], lo["target_lane"])
+            np.testing.assert_array_equal(got["n_out"], lo["n_out"])
+            for k in ["plan_x", "plan_y"]:
+                assert np.abs(got[k] - lo[k]).max() <= TOL, (f, k)
+            new = {k: x.cpu().numpy() for k, x in d.items()}
+            for k in new:
+                if k == "ego_yaw_deg":
+                    np.testing.assert_allclose(new[k], sc[k], rtol=0, atol=1e-9)
+                elif new[k].dtype.kind == "f":
+                    assert np.abs(new[k] - sc[k]).max() <= TOL, (f, k)
+                else:
+                    np.testing.assert_array_equal(new[k], sc[k], err_msg=f"{f} {k}")
+            for k in ["seg", "t"]:
+                np.testing.assert_array_equal(g[k].cpu().numpy(), tr[k])
+
+    def test_large_batch_rollout(self, env):
+        """65,536 scenes x 60 frames: finite, lanes valid, plans full length."""
+        t = env["torch"]
+        S, F = 65536, 60
+        d, g = ppamd.synth_traffic(env["m"], S, seed=12, device=0)
+        prm = ppamd.default_params(n_speeds=1)
+        res = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
+        lg = ppamd.alloc_log(F, S, 50, xp="torch", device=env["dev"], plans=False)
+        ppamd.rollout(env["m"], d, g, prm, res, F, 3, 300.0, lg)
+        t.cuda.synchronize()
+        tl = lg["target_lane"].cpu().numpy()
+        assert ((tl >= 0) & (tl <= 2)).all()
+        assert np.isfinite(lg["ego_x"].cpu().numpy()).all()
+        assert (lg["n_out"].cpu().numpy()[1:] >= 40).mean() > 0.99
