@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--comfort", action="store_true", help="comfort cost mode (data-dependent argmin)")
     ap.add_argument("--draws", type=int, default=0,
                     help="Monte-Carlo sensor-noise draws per scene (config 4: --scenes 16384 --draws 64 --n-speeds 1)")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="closed-loop mode: one step = this many pp_rollout frames (plan + simulator)")
+    ap.add_argument("--sensor-range", type=float, default=300.0)
     ap.add_argument("--seed", type=int, default=0x5EED0001)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -144,12 +147,22 @@ def main():
     m.reserve(local, S * D)
     first, _ = shard(rank, S)
     prm.noise_first_scene = first
-    scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
+    traffic = None
+    if a.rollout:
+        scenes, traffic = ppamd.synth_traffic(m, S, seed=a.seed, first=first, device=local, stream=sp)
+    else:
+        scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
     res = ppamd.alloc_result(S, prm, xp="torch", device=dev)
     torch.cuda.synchronize(dev)
 
+    def step():
+        if a.rollout:
+            ppamd.rollout(m, scenes, traffic, prm, res, a.rollout, 3, a.sensor_range, device=local, stream=sp)
+        else:
+            ppamd.evaluate(m, scenes, prm, res, device=local, stream=sp)
+
     for _ in range(a.warmup):
-        ppamd.evaluate(m, scenes, prm, res, device=local, stream=sp)
+        step()
     torch.cuda.synchronize(dev)
     m.timing(local, True)
     m.read_timing(local)
@@ -158,7 +171,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        ppamd.evaluate(m, scenes, prm, res, device=local, stream=sp)
+        step()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -166,10 +179,11 @@ def main():
     ms, launches = m.read_timing(local)
     m.timing(local, False)
     elapsed = max_over_ranks(elapsed, dist, dev)
-    total_cands = S * Cn * world * a.steps
+    frames = max(a.rollout, 1)
+    total_cands = S * Cn * world * a.steps * frames
     value = total_cands / elapsed
     # dominant kernel: k_cand (HIP events on the launch stream, timed region only)
-    k_cand_ms = ms[1] / max(launches[1], 1)
+    k_cand_ms = ms[1] / max(launches[1], 1)      # per launch (one frame)
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
     bytes_launch = bpc * S * Cn
     achieved = bytes_launch / (k_cand_ms * 1e-3) / 1e9
@@ -186,6 +200,8 @@ def main():
                                 f"BASELINE config 5 batch: {S} scenes x 3 lanes x {a.n_speeds} speeds")
                                + f", {a.n_points}-pt horizon per GPU"
                                + (", all paths emitted" if a.emit_paths else ", winner path + costs")
+                               + (f", closed loop: {a.rollout} frames per step (plan + simulator, 3 points "
+                                  f"driven per frame, sensor range {a.sensor_range:g} m)" if a.rollout else "")
                                + (", comfort cost" if a.comfort else ", reference decision"),
                    "scenes_per_gpu": S, "candidates_per_scene": Cn, "horizon_points": a.n_points,
                    "parallelism": f"scene shards x{world}, no collective"},
@@ -196,7 +212,9 @@ def main():
                      "kernel": "k_cand", "algorithmic_bytes_per_candidate": bpc,
                      "traffic_source": traffic_src},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if a.rollout:
+        out["scene_frames_per_s"] = S * world * a.steps * frames / elapsed
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
         out["cpu_baseline"] = cpu_baseline(m, scenes, prm, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -185,6 +185,7 @@ def test_plan_frame_is_reference_onmessage(env):
         cars = [(int(sc["car_id"][j, s]), sc["car_x"][j, s], sc["car_y"][j, s], sc["car_vx"][j, s],
                  sc["car_vy"][j, s]) for j in range(nc)][::-1]    # any order: sorted by id inside
         npv = int(sc["n_prev"][s])
+        ppamd.plan_reset(env["m"])          # unrelated scenes: no car table carried over
         nx, ny, tl = ppamd.plan_frame(env["m"], sc["ego_x"][s], sc["ego_y"][s], sc["ego_yaw_deg"][s],
                                       sc["ego_speed_mph"][s], sc["prev_x"][:npv, s], sc["prev_y"][:npv, s],
                                       cars, target_lane=int(sc["prev_target_lane"][s]))

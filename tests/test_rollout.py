@@ -141,6 +141,34 @@ class TestRolloutGPU:
             for k in ["seg", "t"]:
                 np.testing.assert_array_equal(g[k].cpu().numpy(), tr[k])
 
+    def test_plan_frame_episode_keeps_car_table(self, env):
+        """pp_plan_frame (the onMessage replacement) over consecutive frames of one episode with
+        cars leaving the sensor range: its persistent table must reproduce the restatement's
+        closed loop (stale entries included) frame after frame."""
+        sc, tr = golden_state("r120")
+        one = {k: np.ascontiguousarray(v[..., :1]) for k, v in sc.items()}
+        tone = {k: (np.ascontiguousarray(v[..., :1]) if isinstance(v, np.ndarray) else v) for k, v in tr.items()}
+        prm = ppamd.default_params(n_speeds=1)
+        ppamd.plan_reset(env["m"])
+        stale_frames = 0
+        for f in range(150):
+            tel = {k: v.copy() for k, v in one.items()}
+            lg = oracle_lib.oracle_rollout(env["olib"], env["wx"], env["wy"], one, tone, prm, 1, 3, 120.0)
+            nc = int(tel["n_cars"][0])
+            cars = [(int(tel["car_id"][j, 0]), tel["car_x"][j, 0], tel["car_y"][j, 0], tel["car_vx"][j, 0],
+                     tel["car_vy"][j, 0]) for j in range(nc)]
+            npv = int(tel["n_prev"][0])
+            nx, ny, tl = ppamd.plan_frame(env["m"], tel["ego_x"][0], tel["ego_y"][0], tel["ego_yaw_deg"][0],
+                                          tel["ego_speed_mph"][0], tel["prev_x"][:min(npv, 10), 0],
+                                          tel["prev_y"][:min(npv, 10), 0], cars,
+                                          target_lane=int(tel["prev_target_lane"][0]))
+            n = int(lg["n_out"][0, 0])
+            assert len(nx) == n and tl == int(lg["target_lane"][0, 0]), f
+            e = max(np.abs(nx - lg["plan_x"][0, :n, 0]).max(initial=0), np.abs(ny - lg["plan_y"][0, :n, 0]).max(initial=0))
+            assert e <= TOL, (f, e)
+            stale_frames += int(one["tab_valid"][:, 0].sum() > nc)
+        assert stale_frames > 0
+
     def test_large_batch_rollout(self, env):
         """65,536 scenes x 60 frames: finite, lanes valid, plans full length."""
         t = env["torch"]
