@@ -110,7 +110,8 @@ class Result(C.Structure):
 EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_create",
            "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
-           "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset"]
+           "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
+           "pp_telemetry_parse", "pp_control_format"]
 
 
 def _load():
@@ -167,6 +168,12 @@ def _load():
     lib.pp_synth_traffic_host.restype = C.c_int32
     lib.pp_plan_reset.argtypes = [C.c_void_p, C.c_int32]
     lib.pp_plan_reset.restype = C.c_int32
+    lib.pp_telemetry_parse.argtypes = [C.c_char_p, C.POINTER(C.c_int64), C.c_int64, C.POINTER(SceneBatch),
+                                       C.POINTER(C.c_int32), C.c_int32]
+    lib.pp_telemetry_parse.restype = C.c_int32
+    lib.pp_control_format.argtypes = [_dp, _dp, C.POINTER(C.c_int32), C.c_int64, C.c_int64, C.c_char_p,
+                                      C.c_int64, C.POINTER(C.c_int64), C.c_int32]
+    lib.pp_control_format.restype = C.c_int32
     return lib
 
 
@@ -493,3 +500,44 @@ def highway_map():
 
 def version() -> str:
     return lib.pp_version().decode()
+
+
+# ---- wire codec (include/pp.h pp_telemetry_parse / pp_control_format; host) ----------------------
+def pack_messages(msgs):
+    """list of bytes -> (contiguous buffer, int64 offsets[n + 1])"""
+    off = np.zeros(len(msgs) + 1, np.int64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    return b"".join(msgs), off
+
+
+def telemetry_parse(msgs, car_stride=MAX_CARS, threads=8):
+    """Socket.io telemetry frames -> (host scene dict, per-message status)."""
+    buf, off = pack_messages(msgs)
+    n = len(msgs)
+    d = alloc_scenes(n, car_stride)
+    st = np.zeros(n, np.int32)
+    b = scene_struct(d)
+    _check(lib.pp_telemetry_parse(buf, off.ctypes.data_as(C.POINTER(C.c_int64)), n, C.byref(b),
+                                  st.ctypes.data_as(C.POINTER(C.c_int32)), threads), "pp_telemetry_parse")
+    return d, st
+
+
+def control_format(next_x, next_y, n_out, threads=8):
+    """Point-major host next_x/next_y [N][S] + n_out -> list of control messages (bytes)."""
+    nx = np.ascontiguousarray(next_x, np.float64)
+    ny = np.ascontiguousarray(next_y, np.float64)
+    no = np.ascontiguousarray(n_out, np.int32)
+    S = no.shape[0]
+    off = np.zeros(S + 1, np.int64)
+    cap = max(1024, S * 2048)
+    while True:
+        out = C.create_string_buffer(cap)
+        rc = lib.pp_control_format(nx.ctypes.data_as(_dp), ny.ctypes.data_as(_dp),
+                                   no.ctypes.data_as(C.POINTER(C.c_int32)), S, nx.shape[-1] if nx.ndim > 1 else S,
+                                   out, cap, off.ctypes.data_as(C.POINTER(C.c_int64)), threads)
+        if rc == -3:
+            cap = int(off[-1]) + 1
+            continue
+        _check(rc, "pp_control_format")
+        raw = out.raw
+        return [raw[off[i]:off[i + 1]] for i in range(S)]

@@ -273,6 +273,25 @@ int32_t pp_synth_traffic_host(const pp_map* m, uint64_t seed, int64_t first_scen
  * in [0, PP_MAX_CARS)); pp_plan_reset empties it (a new episode). */
 int32_t pp_plan_reset(pp_map* m, int32_t device);
 
+/* ---- simulator wire codec (host code) ----------------------------- */
+/* Parses n_msgs socket.io frames `42["telemetry",{...}]` — message m is buf[offsets[m],
+ * offsets[m+1]) — into scenes [0, n_msgs) of a HOST batch (out->n_scenes >= n_msgs), exactly as
+ * the reference's hasData (helpers.h:15-25) + nlohmann::json parse and field reads
+ * (src/main.cpp:1217-1252, 1325-1333) see them: previous_path_x/_y keep their first 10 points and
+ * n_prev = their length; sensor_fusion rows in std::map order (ascending id, last row of an id
+ * wins). msg_status[m]: 0 ok; 1 no data / not telemetry (the reference answers "manual");
+ * 2 parsed but more distinct cars than car_stride (the first car_stride kept); -1 malformed.
+ * n_threads host threads (<= 1: the calling thread). */
+int32_t pp_telemetry_parse(const char* buf, const int64_t* offsets, int64_t n_msgs, pp_scene_batch* out,
+                           int32_t* msg_status, int32_t n_threads);
+/* Formats `42["control",{"next_x":[...],"next_y":[...]}]` per scene from HOST next_x/next_y
+ * ([i * stride + s], the pp_result layout with stride = n_scenes of the batch) and n_out, as
+ * nlohmann::json dump does (%.15g, ".0" for integral values, null for non-finite;
+ * src/main.cpp:1461-1464). Message s is out[offsets[s], offsets[s+1]). Returns PP_ERR_NOMEM with
+ * offsets[n_scenes] = bytes needed when out_cap is too small. */
+int32_t pp_control_format(const double* next_x, const double* next_y, const int32_t* n_out, int64_t n_scenes,
+                          int64_t stride, char* out, int64_t out_cap, int64_t* offsets, int32_t n_threads);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
  * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the
  * summed milliseconds and launch counts per kernel, and clears the record. */

@@ -23,6 +23,7 @@ import ppamd  # noqa: E402  (structures shared with the C-ABI)
 
 ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
 REF_SO = os.path.join(REPO, "oracle", "_ref", "libppref.so")
+REF_JSON_SO = os.path.join(REPO, "oracle", "_ref", "libppref_json.so")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 _dp = C.POINTER(C.c_double)
@@ -186,3 +187,41 @@ class quiet_stdout:
         os.close(self.saved)
         os.close(self.devnull)
         return False
+
+
+def load_ref_json():
+    """The reference's own wire codec (helpers.h hasData + nlohmann json.hpp), or None."""
+    if not os.path.exists(REF_JSON_SO):
+        return None
+    lib = C.CDLL(REF_JSON_SO)
+    ip = C.POINTER(C.c_int)
+    lib.ref_json_parse.argtypes = [C.c_char_p, _dp, _dp, _dp, C.c_int, ip, ip, _dp, C.c_int, ip]
+    lib.ref_json_parse.restype = C.c_int
+    lib.ref_json_dump.argtypes = [_dp, _dp, C.c_int, C.c_char_p, C.c_long]
+    lib.ref_json_dump.restype = C.c_long
+    return lib
+
+
+def ref_json_parse(lib, msg, cap_cars=64):
+    """-> (status, ego[4], prev_x[:10], prev_y[:10], n_prev, ids, cars[n, 4])"""
+    ego = np.zeros(4)
+    px, py = np.zeros(10), np.zeros(10)
+    npv, nc = C.c_int(0), C.c_int(0)
+    ids = np.zeros(cap_cars, np.int32)
+    cars = np.zeros((cap_cars, 4))
+    dp = lambda a: a.ctypes.data_as(_dp)
+    with quiet_stdout():
+        st = lib.ref_json_parse(msg, dp(ego), dp(px), dp(py), 10, C.byref(npv), ids.ctypes.data_as(C.POINTER(C.c_int)),
+                                dp(cars), cap_cars, C.byref(nc))
+    n = min(nc.value, cap_cars)
+    return st, ego, px, py, npv.value, ids[:n], cars[:n]
+
+
+def ref_json_dump(lib, x, y):
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    cap = 64 + 60 * len(x)
+    buf = C.create_string_buffer(cap)
+    n = lib.ref_json_dump(x.ctypes.data_as(_dp), y.ctypes.data_as(_dp), len(x), buf, cap)
+    assert 0 < n <= cap
+    return buf.raw[:n]
