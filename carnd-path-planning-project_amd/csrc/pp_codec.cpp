@@ -258,10 +258,11 @@ bool parse_sensor_fusion(Cur& c, std::vector<Row>& rows) {
     return c.eat(']');
 }
 
-// 0: telemetry parsed; 1: no data / not telemetry (the reference answers "manual"); -1: error
+// 0: telemetry parsed; 1: no data (the reference answers "manual", src/main.cpp:1468-1471);
+// 3: not a "42" event frame or another event (no answer); -1: the reference would throw
 int parse_frame(const char* msg, size_t len, Parsed& P) {
     // src/main.cpp:1220: length > 2 and "42" prefix
-    if (!(len > 2 && msg[0] == '4' && msg[1] == '2')) return 1;
+    if (!(len > 2 && msg[0] == '4' && msg[1] == '2')) return 3;
     // helpers.h:15-25 hasData
     const std::string_view sv(msg, len);
     if (sv.find("null") != std::string_view::npos) return 1;
@@ -273,7 +274,7 @@ int parse_frame(const char* msg, size_t len, Parsed& P) {
     Cur c{msg + b1, msg + end};
     std::string event;
     if (!c.eat('[') || !parse_string(c, &event) || !c.eat(',')) return -1;
-    if (event != "telemetry") { return skip_value(c) && c.eat(']') ? 1 : -1; }
+    if (event != "telemetry") { return skip_value(c) && c.eat(']') ? 3 : -1; }
     if (!c.eat('{')) return -1;
     if (!c.eat('}')) {
         do {

@@ -1023,6 +1023,9 @@ struct DevState {
     void* rec = nullptr;          // reference-mode winner record (per scene)
     int64_t rec_cap = 0;
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
+    void* stage = nullptr;        // pp_plan_batch_host staging buffer
+    size_t stage_cap = 0;
+    std::mutex stage_mu;          // one pp_plan_batch_host at a time per device
     bool table_reset = true;      // pp_plan_frame's persistent car table must be cleared
     struct PlanTab {              // pp_plan_frame's car table (host copy between frames)
         double s[PP_MAX_CARS], d[PP_MAX_CARS], vs[PP_MAX_CARS], vd[PP_MAX_CARS], vx[PP_MAX_CARS], vy[PP_MAX_CARS];
@@ -1272,6 +1275,7 @@ int32_t pp_map_destroy(pp_map* M) {
         if (D.ws) (void)hipFree(D.ws);
         if (D.rec) (void)hipFree(D.rec);
         if (D.frame) (void)hipFree(D.frame);
+        if (D.stage) (void)hipFree(D.stage);
         for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : D.ev_rec) (void)hipEventDestroy(e);
     }
@@ -1545,6 +1549,108 @@ int32_t pp_rollout(pp_map* M, pp_scene_batch* tel, pp_traffic* traffic, const pp
                            tv, *prm, *res, A);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
     }
+    return PP_OK;
+}
+
+// Host-memory batch (the batched onMessage): stage the scenes (and their car table) into device
+// memory, pp_eval, copy results (and the updated table) back. Synchronous.
+int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const pp_params* prm,
+                           pp_result* hout, void* hip_stream) {
+    if (!M || !hin || !prm || !hout || device < 0 || device >= kMaxDev || !params_ok(prm) || prm->emit_paths ||
+        hin->n_scenes < 0 || hin->car_stride < 0 || hin->car_stride > PP_MAX_CARS)
+        return PP_ERR_ARG;
+    if (!hout->winner || !hout->n_out || !hout->next_x || !hout->next_y || !hout->cost || !hout->status)
+        return PP_ERR_ARG;
+    const int64_t S = hin->n_scenes;
+    if (S == 0) return PP_OK;
+    const int J = hin->car_stride, N = prm->n_points;
+    const int C = n_draws(prm) * 3 * prm->n_speeds;
+    const bool tab = hin->tab_valid != nullptr;
+    // staging layout: doubles first, then 4-byte fields
+    const size_t nd = (size_t)S * (4 + 2 * PP_PREV_KEEP + 4 * J + (tab ? 6 * PP_MAX_CARS : 0) + 2 * N + C);
+    const size_t ni = (size_t)S * (3 + J + (tab ? 2 * PP_MAX_CARS : 0) + 3);
+    const size_t bytes = nd * 8 + ni * 4 + 256;
+    DeviceGuard g(device);
+    hipStream_t st = (hipStream_t)hip_stream;
+    std::lock_guard<std::mutex> stage_lock(M->dev[device].stage_mu);
+    char* base;
+    {
+        std::lock_guard<std::mutex> lk(M->mu);
+        int rc = dev_init(M, device);
+        if (rc) return rc;
+        DevState& D = M->dev[device];
+        if (D.stage_cap < bytes) {
+            if (D.stage) { (void)hipDeviceSynchronize(); (void)hipFree(D.stage); D.stage = nullptr; D.stage_cap = 0; }
+            if (hipMalloc(&D.stage, bytes) != hipSuccess) return PP_ERR_NOMEM;
+            D.stage_cap = bytes;
+        }
+        base = (char*)D.stage;
+    }
+    double* dp = (double*)base;
+    int32_t* ip = (int32_t*)(base + nd * 8);
+    auto takeD = [&](size_t n) { double* r = dp; dp += n; return r; };
+    auto takeI = [&](size_t n) { int32_t* r = ip; ip += n; return r; };
+    bool ok = true;
+    auto h2d = [&](void* d, const void* h, size_t n) {
+        if (n && hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st) != hipSuccess) ok = false;
+    };
+    pp_scene_batch B;
+    memset(&B, 0, sizeof(B));
+    B.n_scenes = S; B.car_stride = J;
+    double* ego = takeD(4 * S);
+    B.ego_x = ego; B.ego_y = ego + S; B.ego_yaw_deg = ego + 2 * S; B.ego_speed_mph = ego + 3 * S;
+    h2d(ego, hin->ego_x, 8 * S); h2d(ego + S, hin->ego_y, 8 * S);
+    h2d(ego + 2 * S, hin->ego_yaw_deg, 8 * S); h2d(ego + 3 * S, hin->ego_speed_mph, 8 * S);
+    double* pxy = takeD(2 * PP_PREV_KEEP * S);
+    B.prev_x = pxy; B.prev_y = pxy + PP_PREV_KEEP * S;
+    h2d(pxy, hin->prev_x, 8 * PP_PREV_KEEP * S); h2d(pxy + PP_PREV_KEEP * S, hin->prev_y, 8 * PP_PREV_KEEP * S);
+    double* cars = takeD(4 * (size_t)J * S);
+    B.car_x = cars; B.car_y = cars + J * S; B.car_vx = cars + 2 * J * S; B.car_vy = cars + 3 * J * S;
+    if (J) {
+        h2d(cars, hin->car_x, 8 * J * S); h2d(cars + J * S, hin->car_y, 8 * J * S);
+        h2d(cars + 2 * J * S, hin->car_vx, 8 * J * S); h2d(cars + 3 * J * S, hin->car_vy, 8 * J * S);
+    }
+    double* tabd = nullptr;
+    if (tab) {
+        tabd = takeD(6 * PP_MAX_CARS * S);
+        const double* src[6] = {hin->tab_s, hin->tab_d, hin->tab_vs, hin->tab_vd, hin->tab_vx, hin->tab_vy};
+        double** dst[6] = {&B.tab_s, &B.tab_d, &B.tab_vs, &B.tab_vd, &B.tab_vx, &B.tab_vy};
+        for (int k = 0; k < 6; k++) { *dst[k] = tabd + k * PP_MAX_CARS * S; h2d(*dst[k], src[k], 8 * PP_MAX_CARS * S); }
+    }
+    double* nxy = takeD(2 * (size_t)N * S);
+    double* cost = takeD((size_t)C * S);
+    int32_t* ints = takeI(3 * S);
+    B.n_prev = ints; B.prev_target_lane = ints + S; B.n_cars = ints + 2 * S;
+    h2d(ints, hin->n_prev, 4 * S); h2d(ints + S, hin->prev_target_lane, 4 * S); h2d(ints + 2 * S, hin->n_cars, 4 * S);
+    int32_t* cid = takeI((size_t)J * S);
+    B.car_id = cid;
+    h2d(cid, hin->car_id, 4 * J * S);
+    int32_t* tabi = nullptr;
+    if (tab) {
+        tabi = takeI(2 * PP_MAX_CARS * S);
+        B.tab_valid = tabi; B.tab_lane = tabi + PP_MAX_CARS * S;
+        h2d(tabi, hin->tab_valid, 4 * PP_MAX_CARS * S); h2d(tabi + PP_MAX_CARS * S, hin->tab_lane, 4 * PP_MAX_CARS * S);
+    }
+    int32_t* outi = takeI(3 * S);
+    pp_result R;
+    memset(&R, 0, sizeof(R));
+    R.winner = outi; R.n_out = outi + S; R.status = (uint32_t*)(outi + 2 * S);
+    R.next_x = nxy; R.next_y = nxy + (size_t)N * S; R.cost = cost;
+    if (!ok) return PP_ERR_HIP;
+    int rc = pp_eval(M, &B, prm, &R, device, hip_stream);
+    if (rc != PP_OK) return rc;
+    auto d2h = [&](void* h, const void* d, size_t n) {
+        if (n && hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) ok = false;
+    };
+    d2h(hout->winner, R.winner, 4 * S); d2h(hout->n_out, R.n_out, 4 * S); d2h(hout->status, R.status, 4 * S);
+    d2h(hout->next_x, R.next_x, 8 * (size_t)N * S); d2h(hout->next_y, R.next_y, 8 * (size_t)N * S);
+    d2h(hout->cost, R.cost, 8 * (size_t)C * S);
+    if (tab) {
+        double* dstd[6] = {hin->tab_s, hin->tab_d, hin->tab_vs, hin->tab_vd, hin->tab_vx, hin->tab_vy};
+        for (int k = 0; k < 6; k++) d2h(dstd[k], tabd + k * PP_MAX_CARS * S, 8 * PP_MAX_CARS * S);
+        d2h(hin->tab_valid, tabi, 4 * PP_MAX_CARS * S); d2h(hin->tab_lane, tabi + PP_MAX_CARS * S, 4 * PP_MAX_CARS * S);
+    }
+    if (!ok || hipStreamSynchronize(st) != hipSuccess) return PP_ERR_HIP;
     return PP_OK;
 }
 

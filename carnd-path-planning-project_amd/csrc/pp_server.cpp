@@ -1,0 +1,372 @@
+// pp_server.cpp — the simulator shim: a WebSocket server speaking what the
+// reference's uWS hub speaks (src/main.cpp:1214-1494: text frames carrying socket.io events,
+// `42["telemetry",{...}]` in, `42["control",{...}]` or `42["manual",{}]` out), that batches the
+// frames of every connected client per tick into one pp_plan_batch_host call.
+//
+// RFC 6455 subset: HTTP/1.1 upgrade (Sec-WebSocket-Accept = base64(SHA-1(key + GUID))), masked
+// client frames, fragmented text messages, ping -> pong, close -> close. Per connection the
+// planner's cross-frame state is kept like the reference's lambda captures: the std::map car table
+// and target_lane (= 1 at start, src/main.cpp:1194-1195); the reference holds one set per process,
+// the server one per connection. Replies per frame exactly as the lambda: telemetry -> control,
+// "42" without data -> manual, anything else -> nothing; a frame the reference could not parse
+// (its json::parse / field reads would throw and end the process) closes that connection.
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <deque>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pp.h"
+
+namespace {
+
+// ---- SHA-1 (FIPS 180-4) + base64: the handshake's accept key ----------------------------------
+struct Sha1 {
+    uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    static uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+    void block(const uint8_t* p) {
+        uint32_t w[80];
+        for (int i = 0; i < 16; i++) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+        for (int i = 16; i < 80; i++) w[i] = rol(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+        for (int i = 0; i < 80; i++) {
+            uint32_t f, k;
+            if (i < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+            else if (i < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
+            else if (i < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDCu; }
+            else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+            const uint32_t t = rol(a, 5) + f + e + k + w[i];
+            e = d; d = c; c = rol(b, 30); b = a; a = t;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+    }
+    void digest(const std::string& m, uint8_t out[20]) {
+        std::string p = m;
+        const uint64_t bits = (uint64_t)m.size() * 8;
+        p += (char)0x80;
+        while (p.size() % 64 != 56) p += (char)0;
+        for (int i = 7; i >= 0; i--) p += (char)((bits >> (8 * i)) & 0xFF);
+        for (size_t i = 0; i < p.size(); i += 64) block((const uint8_t*)p.data() + i);
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(h[i] >> (24 - 8 * j));
+    }
+};
+
+std::string base64(const uint8_t* d, size_t n) {
+    static const char* T = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    std::string o;
+    for (size_t i = 0; i < n; i += 3) {
+        uint32_t v = (uint32_t)d[i] << 16 | (i + 1 < n ? (uint32_t)d[i + 1] << 8 : 0) | (i + 2 < n ? d[i + 2] : 0);
+        o += T[(v >> 18) & 63];
+        o += T[(v >> 12) & 63];
+        o += i + 1 < n ? T[(v >> 6) & 63] : '=';
+        o += i + 2 < n ? T[v & 63] : '=';
+    }
+    return o;
+}
+
+std::string ws_accept(const std::string& key) {
+    uint8_t dg[20];
+    Sha1 s;
+    s.digest(key + "258EAFA5-E914-47DA-95CA-C5AB0DC85B11", dg);
+    return base64(dg, 20);
+}
+
+void ws_frame(std::string& out, int opcode, const char* p, size_t n) {
+    out += (char)(0x80 | opcode);
+    if (n < 126) out += (char)n;
+    else if (n < 65536) { out += (char)126; out += (char)(n >> 8); out += (char)(n & 0xFF); }
+    else { out += (char)127; for (int i = 7; i >= 0; i--) out += (char)((uint64_t)n >> (8 * i) & 0xFF); }
+    out.append(p, n);
+}
+
+struct Conn {
+    int fd = -1;
+    bool upgraded = false;
+    bool closing = false;
+    std::string in, out, frag;
+    int frag_op = 0;
+    std::deque<std::string> msgs;   // complete text messages, in order
+    // the reference lambda's captures (src/main.cpp:1194-1195)
+    int32_t target_lane = 1;
+    int32_t tvalid[PP_MAX_CARS] = {0}, tlane[PP_MAX_CARS] = {0};
+    double ts[PP_MAX_CARS] = {0}, td[PP_MAX_CARS] = {0}, tvs[PP_MAX_CARS] = {0}, tvd[PP_MAX_CARS] = {0},
+           tvx[PP_MAX_CARS] = {0}, tvy[PP_MAX_CARS] = {0};
+};
+
+// HTTP upgrade; false = not complete yet; sets c.closing on a bad request
+bool handshake(Conn& c) {
+    const size_t e = c.in.find("\r\n\r\n");
+    if (e == std::string::npos) { if (c.in.size() > 16384) c.closing = true; return false; }
+    std::string req = c.in.substr(0, e);
+    c.in.erase(0, e + 4);
+    std::string key;
+    size_t p = 0;
+    while (p < req.size()) {
+        size_t q = req.find("\r\n", p);
+        if (q == std::string::npos) q = req.size();
+        std::string line = req.substr(p, q - p);
+        const size_t col = line.find(':');
+        if (col != std::string::npos) {
+            std::string name = line.substr(0, col);
+            for (char& ch : name) ch = (char)tolower((unsigned char)ch);
+            if (name == "sec-websocket-key") {
+                size_t a = col + 1;
+                while (a < line.size() && line[a] == ' ') a++;
+                size_t b = line.size();
+                while (b > a && (line[b - 1] == ' ' || line[b - 1] == '\r')) b--;
+                key = line.substr(a, b - a);
+            }
+        }
+        p = q + 2;
+    }
+    if (key.empty()) {
+        c.out += "HTTP/1.1 400 Bad Request\r\nContent-Length: 0\r\nConnection: close\r\n\r\n";
+        c.closing = true;
+        return false;
+    }
+    c.out += "HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\nSec-WebSocket-Accept: " +
+             ws_accept(key) + "\r\n\r\n";
+    c.upgraded = true;
+    return true;
+}
+
+// parse complete frames from c.in
+void ws_read(Conn& c) {
+    for (;;) {
+        const size_t n = c.in.size();
+        if (n < 2) return;
+        const uint8_t* b = (const uint8_t*)c.in.data();
+        const bool fin = b[0] & 0x80;
+        const int op = b[0] & 0x0F;
+        const bool masked = b[1] & 0x80;
+        uint64_t len = b[1] & 0x7F;
+        size_t h = 2;
+        if (len == 126) { if (n < 4) return; len = (uint64_t)b[2] << 8 | b[3]; h = 4; }
+        else if (len == 127) { if (n < 10) return; len = 0; for (int i = 0; i < 8; i++) len = len << 8 | b[2 + i]; h = 10; }
+        if (len > (64u << 20)) { c.closing = true; return; }
+        const size_t mh = masked ? 4 : 0;
+        if (n < h + mh + len) return;
+        std::string pay = c.in.substr(h + mh, (size_t)len);
+        if (masked) for (size_t i = 0; i < pay.size(); i++) pay[i] ^= (char)b[h + (i & 3)];
+        c.in.erase(0, h + mh + (size_t)len);
+        if (op == 8) { ws_frame(c.out, 8, pay.data(), pay.size() < 2 ? pay.size() : 2); c.closing = true; return; }
+        if (op == 9) { ws_frame(c.out, 10, pay.data(), pay.size()); continue; }
+        if (op == 10) continue;
+        if (op == 1 || op == 2) { c.frag = pay; c.frag_op = op; }
+        else if (op == 0) c.frag += pay;
+        else { c.closing = true; return; }
+        if (fin) {
+            if (c.frag_op == 1) c.msgs.push_back(std::move(c.frag));
+            c.frag.clear();
+        }
+    }
+}
+
+void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
+
+}  // namespace
+
+extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t* stop, int32_t* bound_port,
+                            int64_t* stats) {
+    if (!M || !o || o->max_clients < 1 || o->max_clients > 65536 || o->n_speeds < 1 || o->n_speeds > PP_MAX_SPEEDS)
+        return PP_ERR_ARG;
+    const int lfd = socket(AF_INET, SOCK_STREAM, 0);
+    if (lfd < 0) return PP_ERR_ARG;
+    int one = 1;
+    setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a;
+    memset(&a, 0, sizeof(a));
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)o->port);
+    if (inet_pton(AF_INET, o->host ? o->host : "127.0.0.1", &a.sin_addr) != 1 ||
+        bind(lfd, (sockaddr*)&a, sizeof(a)) != 0 || listen(lfd, 128) != 0) {
+        close(lfd);
+        return PP_ERR_ARG;
+    }
+    socklen_t al = sizeof(a);
+    getsockname(lfd, (sockaddr*)&a, &al);
+    if (bound_port) *bound_port = ntohs(a.sin_port);
+    set_nonblock(lfd);
+    pp_params prm;
+    pp_params_default(&prm);
+    prm.n_speeds = o->n_speeds;                  // reference decision: winner = (T, max_speed)
+    std::vector<std::unique_ptr<Conn>> conns;
+    int64_t frames = 0, ticks = 0, accepted = 0, replies = 0;
+    int32_t rc = PP_OK;
+    const int cap = o->max_clients;
+    const int J = PP_MAX_CARS, N = prm.n_points, C = 3 * prm.n_speeds;
+    // host batch (SoA, cap scenes) + results
+    std::vector<double> ego(4 * cap), pxy(2 * PP_PREV_KEEP * cap), cars(4 * J * cap), tabd(6 * PP_MAX_CARS * cap);
+    std::vector<int32_t> ints(3 * cap), cid(J * cap), tabi(2 * PP_MAX_CARS * cap), mst(cap);
+    std::vector<double> nxy(2 * N * cap), cost(C * cap);
+    std::vector<int32_t> win(cap), nout(cap);
+    std::vector<uint32_t> status(cap);
+    std::string obuf;
+    std::vector<int64_t> ooff(cap + 1);
+    while (!(stop && *stop) && rc == PP_OK && !(o->max_frames > 0 && frames >= o->max_frames)) {
+        // poll: listener + connections
+        std::vector<pollfd> pf;
+        pf.push_back({lfd, POLLIN, 0});
+        for (auto& c : conns) pf.push_back({c->fd, (short)(POLLIN | (c->out.empty() ? 0 : POLLOUT)), 0});
+        if (poll(pf.data(), pf.size(), 2) < 0 && errno != EINTR) { rc = PP_ERR_ARG; break; }
+        if (pf[0].revents & POLLIN) {
+            for (;;) {
+                const int fd = accept(lfd, nullptr, nullptr);
+                if (fd < 0) break;
+                if ((int)conns.size() >= cap) { close(fd); continue; }
+                set_nonblock(fd);
+                setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+                auto c = std::make_unique<Conn>();
+                c->fd = fd;
+                conns.push_back(std::move(c));
+                accepted++;
+            }
+        }
+        for (size_t k = 0; k < conns.size() && k + 1 < pf.size(); k++) {
+            Conn& c = *conns[k];
+            if (pf[k + 1].revents & (POLLIN | POLLHUP | POLLERR)) {
+                char b[65536];
+                for (;;) {
+                    const ssize_t r = recv(c.fd, b, sizeof(b), 0);
+                    if (r > 0) { c.in.append(b, (size_t)r); continue; }
+                    if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) c.closing = true;
+                    break;
+                }
+                if (!c.upgraded) handshake(c);
+                if (c.upgraded) ws_read(c);
+            }
+        }
+        // one pending text message per connection per tick
+        std::vector<int> who;
+        std::vector<std::string> batch;
+        for (size_t k = 0; k < conns.size(); k++) {
+            Conn& c = *conns[k];
+            if (!c.msgs.empty() && !c.closing) {
+                who.push_back((int)k);
+                batch.push_back(std::move(c.msgs.front()));
+                c.msgs.pop_front();
+            }
+        }
+        if (!batch.empty()) {
+            ticks++;
+            const int A = (int)batch.size();
+            std::string buf;
+            std::vector<int64_t> off(A + 1, 0);
+            for (int i = 0; i < A; i++) { buf += batch[i]; off[i + 1] = (int64_t)buf.size(); }
+            pp_scene_batch B;
+            memset(&B, 0, sizeof(B));
+            B.n_scenes = A; B.car_stride = J;
+            B.ego_x = ego.data(); B.ego_y = ego.data() + A; B.ego_yaw_deg = ego.data() + 2 * A; B.ego_speed_mph = ego.data() + 3 * A;
+            B.prev_x = pxy.data(); B.prev_y = pxy.data() + PP_PREV_KEEP * A;
+            B.n_prev = ints.data(); B.prev_target_lane = ints.data() + A; B.n_cars = ints.data() + 2 * A;
+            B.car_id = cid.data();
+            B.car_x = cars.data(); B.car_y = cars.data() + J * A; B.car_vx = cars.data() + 2 * J * A; B.car_vy = cars.data() + 3 * J * A;
+            rc = pp_telemetry_parse(buf.data(), off.data(), A, &B, mst.data(), o->threads);
+            if (rc != PP_OK) break;
+            // dense batch of the telemetry frames, with each connection's state
+            std::vector<int> tel;
+            for (int i = 0; i < A; i++) if (mst[i] == 0 || mst[i] == 2) tel.push_back(i);
+            const int T = (int)tel.size();
+            if (T) {
+                // compact in place (tel is increasing, so i <= tel[i])
+                auto mvD = [&](double* base, int rows) {
+                    for (int r = 0; r < rows; r++) for (int i = 0; i < T; i++) base[(size_t)r * T + i] = base[(size_t)r * A + tel[i]];
+                };
+                auto mvI = [&](int32_t* base, int rows) {
+                    for (int r = 0; r < rows; r++) for (int i = 0; i < T; i++) base[(size_t)r * T + i] = base[(size_t)r * A + tel[i]];
+                };
+                mvD(ego.data(), 4); mvD(pxy.data(), 2 * PP_PREV_KEEP); mvD(cars.data(), 4 * J);
+                mvI(ints.data(), 3); mvI(cid.data(), J);
+                pp_scene_batch D = B;
+                D.n_scenes = T;
+                D.ego_x = ego.data(); D.ego_y = ego.data() + T; D.ego_yaw_deg = ego.data() + 2 * T; D.ego_speed_mph = ego.data() + 3 * T;
+                D.prev_x = pxy.data(); D.prev_y = pxy.data() + PP_PREV_KEEP * T;
+                D.n_prev = ints.data(); D.prev_target_lane = ints.data() + T; D.n_cars = ints.data() + 2 * T;
+                D.car_x = cars.data(); D.car_y = cars.data() + J * T; D.car_vx = cars.data() + 2 * J * T; D.car_vy = cars.data() + 3 * J * T;
+                D.tab_valid = tabi.data(); D.tab_lane = tabi.data() + PP_MAX_CARS * T;
+                D.tab_s = tabd.data(); D.tab_d = tabd.data() + PP_MAX_CARS * T; D.tab_vs = tabd.data() + 2 * PP_MAX_CARS * T;
+                D.tab_vd = tabd.data() + 3 * PP_MAX_CARS * T; D.tab_vx = tabd.data() + 4 * PP_MAX_CARS * T;
+                D.tab_vy = tabd.data() + 5 * PP_MAX_CARS * T;
+                for (int i = 0; i < T; i++) {
+                    Conn& c = *conns[who[tel[i]]];
+                    ((int32_t*)D.prev_target_lane)[i] = c.target_lane;
+                    for (int j = 0; j < PP_MAX_CARS; j++) {
+                        const size_t x = (size_t)j * T + i;
+                        D.tab_valid[x] = c.tvalid[j]; D.tab_lane[x] = c.tlane[j]; D.tab_s[x] = c.ts[j]; D.tab_d[x] = c.td[j];
+                        D.tab_vs[x] = c.tvs[j]; D.tab_vd[x] = c.tvd[j]; D.tab_vx[x] = c.tvx[j]; D.tab_vy[x] = c.tvy[j];
+                    }
+                }
+                pp_result R;
+                memset(&R, 0, sizeof(R));
+                R.winner = win.data(); R.n_out = nout.data(); R.next_x = nxy.data(); R.next_y = nxy.data() + (size_t)N * T;
+                R.cost = cost.data(); R.status = status.data();
+                rc = pp_plan_batch_host(M, o->device, &D, &prm, &R, nullptr);
+                if (rc != PP_OK) break;
+                for (int i = 0; i < T; i++) {
+                    Conn& c = *conns[who[tel[i]]];
+                    c.target_lane = win[i] / prm.n_speeds;
+                    for (int j = 0; j < PP_MAX_CARS; j++) {
+                        const size_t x = (size_t)j * T + i;
+                        c.tvalid[j] = D.tab_valid[x]; c.tlane[j] = D.tab_lane[x]; c.ts[j] = D.tab_s[x]; c.td[j] = D.tab_d[x];
+                        c.tvs[j] = D.tab_vs[x]; c.tvd[j] = D.tab_vd[x]; c.tvx[j] = D.tab_vx[x]; c.tvy[j] = D.tab_vy[x];
+                    }
+                }
+                int64_t need = 0;
+                ooff.assign(T + 1, 0);
+                int frc = pp_control_format(R.next_x, R.next_y, R.n_out, T, T, nullptr, 0, ooff.data(), o->threads);
+                need = ooff[T];
+                obuf.resize((size_t)need);
+                frc = pp_control_format(R.next_x, R.next_y, R.n_out, T, T, &obuf[0], need, ooff.data(), o->threads);
+                if (frc != PP_OK) { rc = frc; break; }
+                for (int i = 0; i < T; i++) {
+                    Conn& c = *conns[who[tel[i]]];
+                    ws_frame(c.out, 1, obuf.data() + ooff[i], (size_t)(ooff[i + 1] - ooff[i]));
+                    replies++;
+                }
+                frames += T;
+            }
+            for (int i = 0; i < A; i++) {
+                Conn& c = *conns[who[i]];
+                if (mst[i] == 1) { static const char m[] = "42[\"manual\",{}]"; ws_frame(c.out, 1, m, sizeof(m) - 1); replies++; }
+                else if (mst[i] == -1) c.closing = true;
+            }
+        }
+        // flush, drop closed
+        for (auto& c : conns) {
+            while (!c->out.empty()) {
+                const ssize_t w = send(c->fd, c->out.data(), c->out.size(), MSG_NOSIGNAL);
+                if (w > 0) { c->out.erase(0, (size_t)w); continue; }
+                if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+                c->closing = true;
+                c->out.clear();
+            }
+        }
+        for (size_t k = 0; k < conns.size();) {
+            if (conns[k]->closing && conns[k]->out.empty()) { close(conns[k]->fd); conns.erase(conns.begin() + k); }
+            else k++;
+        }
+    }
+    for (auto& c : conns) close(c->fd);
+    close(lfd);
+    if (stats) { stats[0] = frames; stats[1] = ticks; stats[2] = accepted; stats[3] = replies; }
+    return rc;
+}
+
+extern "C" int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap) {
+    if (!key || !out || cap < 29) return PP_ERR_ARG;
+    const std::string a = ws_accept(key);
+    memcpy(out, a.c_str(), a.size() + 1);
+    return PP_OK;
+}

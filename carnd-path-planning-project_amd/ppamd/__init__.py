@@ -59,6 +59,11 @@ class Traffic(C.Structure):
                 ("t", C.c_void_p), ("offset", C.c_void_p), ("speed", C.c_void_p)]
 
 
+class ServerOpts(C.Structure):
+    _fields_ = [("host", C.c_char_p), ("port", C.c_int32), ("max_clients", C.c_int32), ("n_speeds", C.c_int32),
+                ("threads", C.c_int32), ("device", C.c_int32), ("_pad", C.c_int32), ("max_frames", C.c_int64)]
+
+
 class RolloutCfg(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("consume", C.c_int32), ("sensor_range", C.c_double)]
 
@@ -111,7 +116,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
-           "pp_telemetry_parse", "pp_control_format"]
+           "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key"]
 
 
 def _load():
@@ -174,6 +179,14 @@ def _load():
     lib.pp_control_format.argtypes = [_dp, _dp, C.POINTER(C.c_int32), C.c_int64, C.c_int64, C.c_char_p,
                                       C.c_int64, C.POINTER(C.c_int64), C.c_int32]
     lib.pp_control_format.restype = C.c_int32
+    lib.pp_plan_batch_host.argtypes = [C.c_void_p, C.c_int32, C.POINTER(SceneBatch), C.POINTER(Params),
+                                       C.POINTER(Result), C.c_void_p]
+    lib.pp_plan_batch_host.restype = C.c_int32
+    lib.pp_serve.argtypes = [C.c_void_p, C.POINTER(ServerOpts), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                             C.POINTER(C.c_int64)]
+    lib.pp_serve.restype = C.c_int32
+    lib.pp_ws_accept_key.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
+    lib.pp_ws_accept_key.restype = C.c_int32
     return lib
 
 
@@ -541,3 +554,43 @@ def control_format(next_x, next_y, n_out, threads=8):
         _check(rc, "pp_control_format")
         raw = out.raw
         return [raw[off[i]:off[i + 1]] for i in range(S)]
+
+
+def plan_batch_host(m, scenes, prm, device=0):
+    """pp_plan_batch_host: host scene dict (optionally with a car table, updated in place) ->
+    host result dict (winner, n_out, next_x/next_y [N][S], cost, status)."""
+    S = int(scenes["ego_x"].shape[0])
+    r = alloc_result(S, prm)
+    _check(lib.pp_plan_batch_host(m.handle, device, C.byref(scene_struct(scenes)), C.byref(prm),
+                                  C.byref(result_struct(r)), None), "pp_plan_batch_host")
+    return r
+
+
+class Server:
+    """pp_serve on a background thread (ctypes releases the GIL for the blocking call)."""
+
+    def __init__(self, m, port=0, max_clients=64, n_speeds=1, threads=4, device=0, max_frames=0):
+        import threading
+        self.m = m
+        self.opts = ServerOpts(b"127.0.0.1", port, max_clients, n_speeds, threads, device, 0, max_frames)
+        self.stop_flag = C.c_int32(0)
+        self.port = C.c_int32(0)
+        self.stats = (C.c_int64 * 4)()
+        self.rc = None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+        import time
+        t0 = time.time()
+        while self.port.value == 0 and self.rc is None and time.time() - t0 < 10:
+            time.sleep(0.005)
+        if self.port.value == 0:
+            raise PPError(f"pp_serve did not start (rc={self.rc})")
+
+    def _run(self):
+        self.rc = lib.pp_serve(self.m.handle, C.byref(self.opts), C.byref(self.stop_flag), C.byref(self.port),
+                               self.stats)
+
+    def close(self):
+        self.stop_flag.value = 1
+        self.thread.join(timeout=30)
+        return self.rc, list(self.stats)

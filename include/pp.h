@@ -269,6 +269,13 @@ int32_t pp_synth_traffic(pp_map* m, uint64_t seed, int64_t first_scene, pp_scene
 int32_t pp_synth_traffic_host(const pp_map* m, uint64_t seed, int64_t first_scene,
                               pp_scene_batch* telemetry, pp_traffic* out);
 
+/* A batch in HOST memory (the batched onMessage; what a server calls per tick): stages the
+ * scenes — and their car table when tab_valid is set, updated in place — through device memory,
+ * runs pp_eval on hip_stream and copies winner, n_out, next_x/next_y, cost and status back into
+ * the host pp_result. Synchronous. emit_paths must be 0. */
+int32_t pp_plan_batch_host(pp_map* m, int32_t device, pp_scene_batch* host_in, const pp_params* prm,
+                           pp_result* host_out, void* hip_stream);
+
 /* pp_plan_frame keeps the reference's car table across calls (per map and device, cars with ids
  * in [0, PP_MAX_CARS)); pp_plan_reset empties it (a new episode). */
 int32_t pp_plan_reset(pp_map* m, int32_t device);
@@ -279,9 +286,11 @@ int32_t pp_plan_reset(pp_map* m, int32_t device);
  * the reference's hasData (helpers.h:15-25) + nlohmann::json parse and field reads
  * (src/main.cpp:1217-1252, 1325-1333) see them: previous_path_x/_y keep their first 10 points and
  * n_prev = their length; sensor_fusion rows in std::map order (ascending id, last row of an id
- * wins). msg_status[m]: 0 ok; 1 no data / not telemetry (the reference answers "manual");
- * 2 parsed but more distinct cars than car_stride (the first car_stride kept); -1 malformed.
- * n_threads host threads (<= 1: the calling thread). */
+ * wins). msg_status[m]: 0 telemetry; 1 no data (hasData empty: the reference answers
+ * `42["manual",{}]`); 2 telemetry with more distinct cars than car_stride (the first car_stride
+ * kept); 3 no "42" prefix or another event (the reference does not answer); -1 malformed (the
+ * reference's json::parse or field reads would throw). n_threads host threads (<= 1: the calling
+ * thread). */
 int32_t pp_telemetry_parse(const char* buf, const int64_t* offsets, int64_t n_msgs, pp_scene_batch* out,
                            int32_t* msg_status, int32_t n_threads);
 /* Formats `42["control",{"next_x":[...],"next_y":[...]}]` per scene from HOST next_x/next_y
@@ -291,6 +300,32 @@ int32_t pp_telemetry_parse(const char* buf, const int64_t* offsets, int64_t n_ms
  * offsets[n_scenes] = bytes needed when out_cap is too small. */
 int32_t pp_control_format(const double* next_x, const double* next_y, const int32_t* n_out, int64_t n_scenes,
                           int64_t stride, char* out, int64_t out_cap, int64_t* offsets, int32_t n_threads);
+
+/* ---- simulator shim (host code) ------------------------------------ */
+/* A WebSocket server that speaks what the reference's uWS hub speaks on port 4567
+ * (src/main.cpp:1214-1494): text frames with socket.io events; per frame the lambda's answers
+ * (telemetry -> `42["control",...]`, a "42" frame without data -> `42["manual",{}]`, anything
+ * else -> none). Every tick it takes one pending frame from each connected client and plans all of
+ * them in one pp_plan_batch_host call (reference decision, 3 x n_speeds candidates); each
+ * connection keeps the lambda's cross-frame state (car table, target_lane = 1 at start). */
+typedef struct pp_server_opts {
+    const char* host;              /* "127.0.0.1" (NULL: same)                                    */
+    int32_t port;                  /* 4567 in the reference; 0 = any free port (see bound_port)    */
+    int32_t max_clients;           /* connections served (and batched) at once                     */
+    int32_t n_speeds;              /* 1 = the reference's own 3 candidates                         */
+    int32_t threads;               /* codec threads                                                */
+    int32_t device;
+    int32_t _pad;
+    int64_t max_frames;            /* return after this many telemetry frames (0: until *stop)     */
+} pp_server_opts;
+
+/* Blocking; returns when *stop != 0 (set from another thread) or after max_frames. bound_port
+ * receives the listening port once bound; stats (4): telemetry frames, batches, connections
+ * accepted, replies sent. */
+int32_t pp_serve(pp_map* m, const pp_server_opts* opts, volatile int32_t* stop, int32_t* bound_port,
+                 int64_t* stats);
+/* RFC 6455 Sec-WebSocket-Accept for a client key (the handshake's known-answer check). */
+int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
  * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the

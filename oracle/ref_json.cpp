@@ -17,18 +17,19 @@
 
 using nlohmann::json;
 
-// 0: telemetry; 1: no data / other event (manual); -1: the reference would throw
+// 0: telemetry; 1: no data (manual answer); 3: not a "42" frame / other event (no answer);
+// -1: the reference would throw
 extern "C" int ref_json_parse(const char* msg, double* ego4, double* prev_x, double* prev_y, int cap_prev,
                               int* n_prev, int* ids, double* cars4, int cap_cars, int* n_cars) {
     std::string data(msg);
     const size_t length = data.size();
-    if (!(length && length > 2 && data[0] == '4' && data[1] == '2')) return 1;
+    if (!(length && length > 2 && data[0] == '4' && data[1] == '2')) return 3;
     auto s = hasData(data);
     if (s == "") return 1;
     try {
         auto j = json::parse(s);
         std::string event = j[0].get<std::string>();
-        if (event != "telemetry") return 1;
+        if (event != "telemetry") return 3;
         double ego_x = j[1]["x"];
         double ego_y = j[1]["y"];
         double ego_yaw = j[1]["yaw"];

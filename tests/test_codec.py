@@ -53,7 +53,7 @@ def test_parse_matches_reference_fixture(threads):
         ref = (int(G["status"][s]), G["ego"][s], G["prev_x"][s], G["prev_y"][s], int(G["n_prev"][s]),
                G["car_id"][s][:n], G["cars"][s][:n])
         check_frame(d, st, s, ref)
-    assert (st == 0).sum() > 300 and (st == 1).sum() > 10 and (st == -1).sum() > 5
+    assert (st == 0).sum() > 300 and (st == 1).sum() > 5 and (st == 3).sum() > 5 and (st == -1).sum() > 5
 
 
 def test_format_matches_reference_fixture():
