@@ -8,14 +8,14 @@
 //     payload is [first '[', first '}' + 1];
 //   - numbers (json.hpp:2600-2650): an integer literal is read by strtoull / strtoll and
 //     converted to double (so "-0" gives +0.0, and a 20-digit integer rounds once); any other
-//     literal by strtod. A short-digit fast path (<= 15 significant digits, |exp10| <= 22:
-//     one exactly rounded IEEE operation on exact operands, Clinger 1990) gives the same bits;
-//     everything else calls strtod;
+//     literal by strtod — here the exact integer algorithm of pp_numfmt.h for <= 19 significant
+//     digits and |exp10| <= 27 (the same bits), strtod beyond;
 //   - `int id = car_data[0]`: static_cast<int> of the stored integer or double;
 //   - sensor_fusion rows go into std::map<int, Car> order: ascending id, a repeated id keeps
 //     the last row (src/main.cpp:1329);
-//   - dump (json.hpp:6680-6730): "%.15g" (digits10), ".0" appended when the text has neither
-//     '.' nor 'e', non-finite -> null; object keys in std::map order (next_x < next_y).
+//   - dump (json.hpp:6680-6730): "%.15g" (digits10; pp_numfmt.h fmt15g for 1e-13 <= |x| < 1e18,
+//     snprintf beyond), ".0" appended when the text has neither '.' nor 'e', non-finite -> null;
+//     object keys in std::map order (next_x < next_y).
 // Batches are split over host threads; the product path stays the HIP kernels.
 #include <errno.h>
 #include <math.h>
@@ -30,288 +30,63 @@
 #include <vector>
 
 #include "../../include/pp.h"
+#define PP_HD
+#include "pp_jsonparse.h"
 
 namespace {
 
-struct Cur {
-    const char* p;
-    const char* e;
-    bool ok = true;
-    void ws() {
-        while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++;
-    }
-    bool eat(char c) {
-        ws();
-        if (p < e && *p == c) { p++; return true; }
-        return false;
-    }
-    bool peek(char c) {
-        ws();
-        return p < e && *p == c;
-    }
+struct HostReader {
+    const char* b;
+    int at(int64_t i) const { return (unsigned char)b[i]; }
 };
 
-// 10^k, k <= 22: exact doubles
-const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-
-// A JSON number as nlohmann 2.1 reads it. kind: 0 unsigned integer, 1 signed integer, 2 float
-struct Num {
-    double d;
-    int64_t i;
-    uint64_t u;
-    int kind;
-};
-
-bool parse_number(Cur& c, Num& out) {
-    c.ws();
-    const char* s = c.p;
-    const char* p = s;
-    const char* e = c.e;
-    bool neg = false;
-    if (p < e && *p == '-') { neg = true; p++; }
-    if (p >= e || *p < '0' || *p > '9') return false;
-    const char* int_b = p;
-    if (*p == '0') p++;
-    else while (p < e && *p >= '0' && *p <= '9') p++;
-    const char* int_e = p;
-    const char* frac_b = nullptr;
-    const char* frac_e = nullptr;
-    bool is_float = false;
-    if (p < e && *p == '.') {
-        p++;
-        frac_b = p;
-        if (p >= e || *p < '0' || *p > '9') return false;
-        while (p < e && *p >= '0' && *p <= '9') p++;
-        frac_e = p;
-        is_float = true;
-    }
-    int exp10 = 0;
-    bool exp_big = false;
-    if (p < e && (*p == 'e' || *p == 'E')) {
-        p++;
-        bool eneg = false;
-        if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; p++; }
-        if (p >= e || *p < '0' || *p > '9') return false;
-        while (p < e && *p >= '0' && *p <= '9') {
-            if (exp10 < 100000) exp10 = exp10 * 10 + (*p - '0');
-            else exp_big = true;
-            p++;
-        }
-        if (eneg) exp10 = -exp10;
-        is_float = true;
-    }
-    c.p = p;
-    const size_t len = (size_t)(p - s);
-    char small[72];
-    std::string big;
-    const char* z;                  // NUL-terminated copy for the libc conversions
-    if (len < sizeof(small)) { memcpy(small, s, len); small[len] = 0; z = small; }
-    else { big.assign(s, len); z = big.c_str(); }
-    if (!is_float) {
-        // json.hpp:2600-2630: strtoull / strtoll first; on overflow fall through to strtod
-        char* endp = nullptr;
-        errno = 0;
-        if (!neg) {
-            const unsigned long long x = strtoull(z, &endp, 10);
-            if (errno == 0) { out.kind = 0; out.u = (uint64_t)x; out.d = (double)out.u; return true; }
-        } else {
-            const long long x = strtoll(z, &endp, 10);
-            if (errno == 0) { out.kind = 1; out.i = (int64_t)x; out.d = (double)out.i; return true; }
-        }
-    }
-    out.kind = 2;
-    // fast path: <= 15 significant digits, |effective exponent| <= 22 -> one exact IEEE op
-    if (!exp_big) {
-        uint64_t m = 0;
-        int nd = 0;                 // significant digits accumulated
-        bool lead = true;
-        bool fits = true;
-        for (const char* q = int_b; q < int_e; q++) {
-            if (lead && *q == '0') continue;
-            lead = false;
-            if (++nd > 15) { fits = false; break; }
-            m = m * 10 + (uint64_t)(*q - '0');
-        }
-        int e10 = exp10;
-        if (fits && frac_b) {
-            for (const char* q = frac_b; q < frac_e; q++) {
-                e10--;
-                if (lead && *q == '0') continue;
-                lead = false;
-                if (++nd > 15) { fits = false; break; }
-                m = m * 10 + (uint64_t)(*q - '0');
-            }
-        }
-        if (fits && e10 >= -22 && e10 <= 22) {
-            double v = (double)m;
-            v = e10 >= 0 ? v * kPow10[e10] : v / kPow10[-e10];
-            out.d = neg ? -v : v;
-            return true;
-        }
-    }
-    out.d = strtod(z, nullptr);
-    return true;
-}
-
-bool parse_string(Cur& c, std::string* out) {
-    if (!c.eat('"')) return false;
-    const char* b = c.p;
-    while (c.p < c.e && *c.p != '"') {
-        if (*c.p == '\\') { c.p++; if (c.p >= c.e) return false; }
-        c.p++;
-    }
-    if (c.p >= c.e) return false;
-    if (out) out->assign(b, (size_t)(c.p - b));
-    c.p++;
-    return true;
-}
-
-bool skip_value(Cur& c, int depth = 0) {
-    if (depth > 64) return false;
-    c.ws();
-    if (c.p >= c.e) return false;
-    const char ch = *c.p;
-    if (ch == '"') return parse_string(c, nullptr);
-    if (ch == '{') {
-        c.p++;
-        if (c.eat('}')) return true;
-        do {
-            if (!parse_string(c, nullptr) || !c.eat(':') || !skip_value(c, depth + 1)) return false;
-        } while (c.eat(','));
-        return c.eat('}');
-    }
-    if (ch == '[') {
-        c.p++;
-        if (c.eat(']')) return true;
-        do {
-            if (!skip_value(c, depth + 1)) return false;
-        } while (c.eat(','));
-        return c.eat(']');
-    }
-    auto lit = [&](const char* w) {
-        const size_t n = strlen(w);
-        if ((size_t)(c.e - c.p) >= n && memcmp(c.p, w, n) == 0) { c.p += n; return true; }
-        return false;
-    };
-    if (ch == 't') return lit("true");
-    if (ch == 'f') return lit("false");
-    if (ch == 'n') return lit("null");
-    Num x;
-    return parse_number(c, x);
-}
-
-// array of numbers; the first `keep` values are stored
-bool parse_num_array(Cur& c, double* dst, int keep, int32_t* count) {
-    if (!c.eat('[')) return false;
-    int n = 0;
-    if (!c.eat(']')) {
-        do {
-            Num x;
-            if (!parse_number(c, x)) return false;
-            if (n < keep) dst[n] = x.d;
-            n++;
-        } while (c.eat(','));
-        if (!c.eat(']')) return false;
-    }
-    *count = n;
-    return true;
-}
-
-int to_int(const Num& x) {                // nlohmann get<int>: static_cast from the stored type
-    if (x.kind == 0) return (int)x.u;
-    if (x.kind == 1) return (int)x.i;
-    if (!(x.d > -2147483649.0 && x.d < 2147483648.0)) return INT32_MIN;   // UB in the reference
-    return (int)x.d;
-}
-
-struct Row { int id; double x, y, vx, vy; };
-
-struct Parsed {
+// fields of one frame; numbers outside pp_numfmt's domain go through libc like nlohmann's
+struct HostSink {
     double x = 0, y = 0, yaw = 0, speed = 0;
     double px[PP_PREV_KEEP], py[PP_PREV_KEEP];
     int32_t npx = 0, npy = 0;
-    std::vector<Row> rows;
-    bool has[6] = {false, false, false, false, false, false};
-    bool has_sf = false;
+    std::vector<int> id;
+    std::vector<double> cx, cy, cvx, cvy;
+    void reset() { npx = npy = 0; id.clear(); cx.clear(); cy.clear(); cvx.clear(); cvy.clear(); }
+    void scalar(int f, double v) { (f == 0 ? x : f == 1 ? y : f == 2 ? yaw : speed) = v; }
+    void prev(int which, int i, double v) { if (i < PP_PREV_KEEP) (which ? py : px)[i] = v; }
+    void prev_count(int which, int n) { (which ? npy : npx) = n; }
+    void row(int i, double a, double b, double c, double d) { id.push_back(i); cx.push_back(a); cy.push_back(b); cvx.push_back(c); cvy.push_back(d); }
+    bool host_needed() const { return false; }
+    // json.hpp:2600-2650: strtoull / strtoll for integer tokens (then strtod on overflow), strtod
+    bool slow_number(const HostReader& r, int64_t s, int64_t q, bool is_int, bool neg, ppjson::Num& out) {
+        std::string z(r.b + s, (size_t)(q - s));
+        if (is_int) {
+            char* endp = nullptr;
+            errno = 0;
+            if (!neg) {
+                const unsigned long long v = strtoull(z.c_str(), &endp, 10);
+                if (errno == 0) { out.kind = 0; out.u = (uint64_t)v; out.d = (double)out.u; return true; }
+            } else {
+                const long long v = strtoll(z.c_str(), &endp, 10);
+                if (errno == 0) { out.kind = 1; out.i = (int64_t)v; out.d = (double)out.i; return true; }
+            }
+        }
+        out.kind = 2;
+        out.d = strtod(z.c_str(), nullptr);
+        return true;
+    }
 };
 
-bool parse_sensor_fusion(Cur& c, std::vector<Row>& rows) {
-    if (!c.eat('[')) return false;
-    if (c.eat(']')) return true;
-    do {
-        if (!c.eat('[')) return false;
-        Num v[5];
-        int n = 0;
-        if (!c.eat(']')) {
-            do {
-                Num x;
-                if (!parse_number(c, x)) return false;
-                if (n < 5) v[n] = x;
-                n++;
-            } while (c.eat(','));
-            if (!c.eat(']')) return false;
-        }
-        if (n < 5) return false;          // car_data[1..4] must exist
-        rows.push_back({to_int(v[0]), v[1].d, v[2].d, v[3].d, v[4].d});
-    } while (c.eat(','));
-    return c.eat(']');
-}
-
-// 0: telemetry parsed; 1: no data (the reference answers "manual", src/main.cpp:1468-1471);
-// 3: not a "42" event frame or another event (no answer); -1: the reference would throw
-int parse_frame(const char* msg, size_t len, Parsed& P) {
-    // src/main.cpp:1220: length > 2 and "42" prefix
-    if (!(len > 2 && msg[0] == '4' && msg[1] == '2')) return 3;
-    // helpers.h:15-25 hasData
-    const std::string_view sv(msg, len);
-    if (sv.find("null") != std::string_view::npos) return 1;
-    const size_t b1 = sv.find_first_of('['), b2 = sv.find_first_of('}');
-    if (b1 == std::string_view::npos || b2 == std::string_view::npos) return 1;
-    size_t end = b2 + 2;
-    if (end > len) end = len;
-    if (end < b1) return -1;
-    Cur c{msg + b1, msg + end};
-    std::string event;
-    if (!c.eat('[') || !parse_string(c, &event) || !c.eat(',')) return -1;
-    if (event != "telemetry") { return skip_value(c) && c.eat(']') ? 3 : -1; }
-    if (!c.eat('{')) return -1;
-    if (!c.eat('}')) {
-        do {
-            std::string key;
-            if (!parse_string(c, &key) || !c.eat(':')) return -1;
-            // a repeated key keeps its first value (json.hpp:3084 object emplace)
-            Num x;
-            double* scal[4] = {&P.x, &P.y, &P.yaw, &P.speed};
-            const int k = key == "x" ? 0 : key == "y" ? 1 : key == "yaw" ? 2 : key == "speed" ? 3
-                        : key == "previous_path_x" ? 4 : key == "previous_path_y" ? 5
-                        : key == "sensor_fusion" ? 6 : -1;
-            if (k >= 0 && k < 6 && P.has[k]) { if (!skip_value(c)) return -1; continue; }
-            if (k == 6 && P.has_sf) { if (!skip_value(c)) return -1; continue; }
-            if (k >= 0 && k < 4) { if (!parse_number(c, x)) return -1; *scal[k] = x.d; P.has[k] = true; }
-            else if (k == 4) { if (!parse_num_array(c, P.px, PP_PREV_KEEP, &P.npx)) return -1; P.has[4] = true; }
-            else if (k == 5) { if (!parse_num_array(c, P.py, PP_PREV_KEEP, &P.npy)) return -1; P.has[5] = true; }
-            else if (k == 6) { if (!parse_sensor_fusion(c, P.rows)) return -1; P.has_sf = true; }
-            else if (!skip_value(c)) return -1;
-        } while (c.eat(','));
-        if (!c.eat('}')) return -1;
+struct HostWriter {
+    std::string& o;
+    void put(char c) { o += c; }
+    void put(const char* p, int n) { o.append(p, (size_t)n); }
+    bool slow_number(double x) {
+        char b[64];
+        const int n = snprintf(b, sizeof(b), "%.15g", x);
+        o.append(b, (size_t)n);
+        bool int_like = true;
+        for (int i = 0; i < n; i++) if (b[i] == '.' || b[i] == 'e') { int_like = false; break; }
+        if (int_like) o += ".0";
+        return true;
     }
-    if (!c.eat(']')) return -1;
-    for (bool h : P.has) if (!h) return -1;
-    if (P.npx != P.npy) return -1;
-    return 0;
-}
-
-// "%.15g" + ".0" when int-like; null when not finite (json.hpp:6680-6730)
-inline void dump_float(std::string& o, double x) {
-    if (!std::isfinite(x)) { o += "null"; return; }
-    char b[64];
-    const int n = snprintf(b, sizeof(b), "%.15g", x);
-    o.append(b, (size_t)n);
-    bool int_like = true;
-    for (int i = 0; i < n; i++) if (b[i] == '.' || b[i] == 'e') { int_like = false; break; }
-    if (int_like) o += ".0";
-}
+};
 
 template <class F>
 void parallel_for(int64_t n, int threads, F f) {
@@ -342,44 +117,43 @@ int32_t pp_telemetry_parse(const char* buf, const int64_t* offsets, int64_t n_ms
     const int64_t S = out->n_scenes;
     const int stride = out->car_stride;
     parallel_for(n_msgs, n_threads, [&](int64_t b, int64_t e) {
-        Parsed P;
+        HostSink K;
         for (int64_t s = b; s < e; s++) {
-            P.rows.clear();
-            for (bool& h : P.has) h = false;
-            P.has_sf = false;
-            P.npx = P.npy = 0;
+            K.reset();
             const int64_t o0 = offsets[s], o1 = offsets[s + 1];
-            int st = o1 >= o0 ? parse_frame(buf + o0, (size_t)(o1 - o0), P) : -1;
-            // std::map<int, Car> order: ascending id, the last row of an id wins
-            std::stable_sort(P.rows.begin(), P.rows.end(), [](const Row& a, const Row& c) { return a.id < c.id; });
-            std::vector<Row> u;
-            for (size_t k = 0; k < P.rows.size(); k++) {
-                if (k + 1 < P.rows.size() && P.rows[k + 1].id == P.rows[k].id) continue;
-                u.push_back(P.rows[k]);
+            int st = ppjson::kMsgBad;
+            if (o1 >= o0) {
+                HostReader R{buf + o0};
+                st = ppjson::parse_frame(R, o1 - o0, K);
+                if (st == ppjson::kMsgOk && K.npx != K.npy) st = ppjson::kMsgBad;
             }
-            if (st == 0 && (int)u.size() > stride) st = 2;     // more distinct cars than columns
+            int u = 0;
+            if (st == ppjson::kMsgOk) {
+                u = ppjson::map_order(K.id.data(), K.cx.data(), K.cy.data(), K.cvx.data(), K.cvy.data(), (int)K.id.size());
+                if (u > stride) st = ppjson::kMsgTooManyCars;
+            }
+            const bool ok = st == ppjson::kMsgOk || st == ppjson::kMsgTooManyCars;
             msg_status[s] = st;
-            double* ex = (double*)out->ego_x;
-            ex[s] = st >= 0 ? P.x : 0;
-            ((double*)out->ego_y)[s] = st >= 0 ? P.y : 0;
-            ((double*)out->ego_yaw_deg)[s] = st >= 0 ? P.yaw : 0;
-            ((double*)out->ego_speed_mph)[s] = st >= 0 ? P.speed : 0;
-            const int np = st >= 0 ? P.npx : 0;
+            ((double*)out->ego_x)[s] = ok ? K.x : 0;
+            ((double*)out->ego_y)[s] = ok ? K.y : 0;
+            ((double*)out->ego_yaw_deg)[s] = ok ? K.yaw : 0;
+            ((double*)out->ego_speed_mph)[s] = ok ? K.speed : 0;
+            const int np = ok ? K.npx : 0;
             ((int32_t*)out->n_prev)[s] = np;
             for (int i = 0; i < PP_PREV_KEEP; i++) {
-                ((double*)out->prev_x)[(int64_t)i * S + s] = i < np ? P.px[i] : 0.0;
-                ((double*)out->prev_y)[(int64_t)i * S + s] = i < np ? P.py[i] : 0.0;
+                ((double*)out->prev_x)[(int64_t)i * S + s] = i < np ? K.px[i] : 0.0;
+                ((double*)out->prev_y)[(int64_t)i * S + s] = i < np ? K.py[i] : 0.0;
             }
-            const int nc = st >= 0 ? std::min((int)u.size(), stride) : 0;
+            const int nc = ok ? std::min(u, stride) : 0;
             ((int32_t*)out->n_cars)[s] = nc;
             for (int j = 0; j < stride; j++) {
                 const int64_t ix = (int64_t)j * S + s;
-                const bool ok = j < nc;
-                ((int32_t*)out->car_id)[ix] = ok ? u[j].id : 0;
-                ((double*)out->car_x)[ix] = ok ? u[j].x : 0.0;
-                ((double*)out->car_y)[ix] = ok ? u[j].y : 0.0;
-                ((double*)out->car_vx)[ix] = ok ? u[j].vx : 0.0;
-                ((double*)out->car_vy)[ix] = ok ? u[j].vy : 0.0;
+                const bool on = j < nc;
+                ((int32_t*)out->car_id)[ix] = on ? K.id[j] : 0;
+                ((double*)out->car_x)[ix] = on ? K.cx[j] : 0.0;
+                ((double*)out->car_y)[ix] = on ? K.cy[j] : 0.0;
+                ((double*)out->car_vx)[ix] = on ? K.cvx[j] : 0.0;
+                ((double*)out->car_vy)[ix] = on ? K.cvy[j] : 0.0;
             }
         }
     });
@@ -395,13 +169,10 @@ int32_t pp_control_format(const double* next_x, const double* next_y, const int3
     parallel_for(n_scenes, n_threads, [&](int64_t b, int64_t e) {
         for (int64_t s = b; s < e; s++) {
             std::string& o = parts[(size_t)s];
+            o.clear();
             o.reserve(2048);
-            o = "42[\"control\",{\"next_x\":[";
-            const int n = n_out[s] < 0 ? 0 : n_out[s];
-            for (int i = 0; i < n; i++) { if (i) o += ','; dump_float(o, next_x[(int64_t)i * stride + s]); }
-            o += "],\"next_y\":[";
-            for (int i = 0; i < n; i++) { if (i) o += ','; dump_float(o, next_y[(int64_t)i * stride + s]); }
-            o += "]}]";
+            HostWriter W{o};
+            ppjson::control_message(W, next_x + s, next_y + s, stride, n_out[s] < 0 ? 0 : n_out[s]);
         }
     });
     int64_t total = 0;
