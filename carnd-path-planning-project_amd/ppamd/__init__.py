@@ -116,7 +116,8 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_map_destroy", "pp_map_geometry", "pp_reserve", "pp_eval", "pp_plan_frame",
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
-           "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key"]
+           "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
+           "pp_telemetry_parse_device", "pp_control_format_device"]
 
 
 def _load():
@@ -187,6 +188,12 @@ def _load():
     lib.pp_serve.restype = C.c_int32
     lib.pp_ws_accept_key.argtypes = [C.c_char_p, C.c_char_p, C.c_int32]
     lib.pp_ws_accept_key.restype = C.c_int32
+    lib.pp_telemetry_parse_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(SceneBatch), C.c_void_p,
+                                              C.c_int32, C.c_void_p]
+    lib.pp_telemetry_parse_device.restype = C.c_int32
+    lib.pp_control_format_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+                                             C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.pp_control_format_device.restype = C.c_int32
     return lib
 
 
@@ -594,3 +601,51 @@ class Server:
         self.stop_flag.value = 1
         self.thread.join(timeout=30)
         return self.rc, list(self.stats)
+
+
+MSG_HOST = 4                      # device codec: the frame needs the host codec
+
+
+def upload_messages(msgs, device=0):
+    """Frames -> (16-byte aligned padded uint8 device buffer, int64 device offsets)."""
+    import torch
+    buf, off = pack_messages(msgs)
+    n = (len(buf) + 15) // 16 * 16 + 16
+    host = np.zeros(n, np.uint8)
+    host[:len(buf)] = np.frombuffer(buf, np.uint8)
+    dev = torch.device("cuda", device)
+    return torch.from_numpy(host).to(dev), torch.from_numpy(off).to(dev)
+
+
+def telemetry_parse_device(msgs, car_stride=MAX_CARS, device=0, stream=None, d_buf=None, d_off=None):
+    """pp_telemetry_parse_device -> (device scene dict, device status)."""
+    import torch
+    dev = torch.device("cuda", device)
+    if d_buf is None:
+        d_buf, d_off = upload_messages(msgs, device)
+    n = int(d_off.shape[0]) - 1
+    d = alloc_scenes(n, car_stride, xp="torch", device=dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    b = scene_struct(d)
+    _check(lib.pp_telemetry_parse_device(d_buf.data_ptr(), d_off.data_ptr(), n, C.byref(b), st.data_ptr(), device,
+                                         stream), "pp_telemetry_parse_device")
+    return d, st
+
+
+def control_format_device(next_x, next_y, n_out, slot_bytes=2560, device=0, stream=None):
+    """pp_control_format_device on torch [N][S] tensors -> (slots uint8 [S, slot_bytes], len int32 [S])."""
+    import torch
+    S = int(n_out.shape[0])
+    slots = torch.empty((S, slot_bytes), dtype=torch.uint8, device=next_x.device)
+    ln = torch.empty(S, dtype=torch.int32, device=next_x.device)
+    _check(lib.pp_control_format_device(next_x.data_ptr(), next_y.data_ptr(), n_out.data_ptr(), S,
+                                        int(next_x.shape[-1]), slots.data_ptr(), slot_bytes, ln.data_ptr(), device,
+                                        stream), "pp_control_format_device")
+    return slots, ln
+
+
+def slots_to_messages(slots, lens):
+    """Host copies of device slots -> list of bytes (None where the host codec must format)."""
+    sl = slots if isinstance(slots, np.ndarray) else slots.cpu().numpy()
+    ln = lens if isinstance(lens, np.ndarray) else lens.cpu().numpy()
+    return [bytes(sl[i, :ln[i]]) if ln[i] >= 0 else None for i in range(len(ln))]

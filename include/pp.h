@@ -301,6 +301,20 @@ int32_t pp_telemetry_parse(const char* buf, const int64_t* offsets, int64_t n_ms
 int32_t pp_control_format(const double* next_x, const double* next_y, const int32_t* n_out, int64_t n_scenes,
                           int64_t stride, char* out, int64_t out_cap, int64_t* offsets, int32_t n_threads);
 
+/* The same codec on the GPU (one lane per frame; identical parser, number conversions and
+ * writer). d_buf: the frames back to back in device memory, 16-byte aligned and readable up to
+ * offsets[n] rounded up to 16; d_out: a DEVICE batch (n_scenes >= n_msgs). Statuses as above,
+ * plus 4: the frame needs the host codec (a number outside the exact conversions' domain, more
+ * than 24 sensor_fusion rows) — its fields are not written. Asynchronous on hip_stream. */
+int32_t pp_telemetry_parse_device(const char* d_buf, const int64_t* d_offsets, int64_t n_msgs, pp_scene_batch* d_out,
+                                  int32_t* d_status, int32_t device, void* hip_stream);
+/* Control messages on the GPU into fixed slots: message s = d_slots[s * slot_bytes, + d_len[s]);
+ * d_len[s] = -1 when the host codec must format it (a number outside fmt15g's domain, or the
+ * slot too small). slot_bytes a multiple of 16; d_slots 16-byte aligned. Asynchronous. */
+int32_t pp_control_format_device(const double* d_next_x, const double* d_next_y, const int32_t* d_n_out,
+                                 int64_t n_scenes, int64_t stride, char* d_slots, int64_t slot_bytes,
+                                 int32_t* d_len, int32_t device, void* hip_stream);
+
 /* ---- simulator shim (host code) ------------------------------------ */
 /* A WebSocket server that speaks what the reference's uWS hub speaks on port 4567
  * (src/main.cpp:1214-1494): text frames with socket.io events; per frame the lambda's answers

@@ -111,3 +111,72 @@ def test_parse_and_format_vs_reference_live(seed):
         x, y = rng.choice(vals, n), rng.choice(vals, n)
         got = ppamd.control_format(x[:, None], y[:, None], np.array([n], np.int32))[0]
         assert got == oracle_lib.ref_json_dump(rj, x, y)
+
+
+@pytest.mark.gpu
+class TestDeviceCodec:
+    """The GPU codec (pp_codec.hip) against the host codec: same statuses (the device hands frames
+    with libc-only numbers to the host: status 4), same bits, same bytes."""
+
+    def compare_parse(self, msgs):
+        hd, hs = ppamd.telemetry_parse(msgs, car_stride=16)
+        dd, ds = ppamd.telemetry_parse_device(msgs, car_stride=16)
+        dd = {k: v.cpu().numpy() for k, v in dd.items()}
+        ds = ds.cpu().numpy()
+        host = ds == ppamd.MSG_HOST
+        assert ((ds == hs) | (host & np.isin(hs, [0, 2]))).all()
+        ok = ~host & np.isin(hs, [0, 2])
+        for k in hd:
+            a, b = np.asarray(hd[k])[..., ok], dd[k][..., ok]
+            if a.dtype.kind == "f":
+                assert (a.view(np.uint64) == b.view(np.uint64)).all(), k
+            else:
+                assert (a == b).all(), k
+        return int(ok.sum()), int(host.sum())
+
+    def test_parse_golden_and_random(self):
+        # adversarial spellings: most frames hold some >19-digit number and go to the host codec
+        n_ok, n_host = self.compare_parse(golden_msgs())
+        assert n_ok > 0 and n_host > 0
+        for seed in (31, 32):
+            self.compare_parse(codec_corpus.corpus(seed, 3000))
+
+    def test_parse_simulator_like_frames_on_device(self):
+        """Frames as a simulator writes them (shortest round-trip numbers): all parsed on the GPU."""
+        import sys
+        import os
+        sys.path.insert(0, os.path.join(oracle_lib.REPO, "tools"))
+        from bench_serving import frames_from_scenes
+        m = ppamd.Map(*oracle_lib.highway_map())
+        msgs = frames_from_scenes(ppamd.synth_host(m, 2000, seed=9))
+        n_ok, n_host = self.compare_parse(msgs)
+        assert n_ok == 2000 and n_host == 0
+
+    def format_both(self, xs, ys, n_out):
+        import torch
+        want = ppamd.control_format(xs, ys, n_out)
+        dev = torch.device("cuda", 0)
+        slots, ln = ppamd.control_format_device(torch.from_numpy(xs).to(dev), torch.from_numpy(ys).to(dev),
+                                                torch.from_numpy(n_out).to(dev))
+        got = ppamd.slots_to_messages(slots, ln)
+        n_dev = 0
+        for s in range(len(want)):
+            if got[s] is not None:
+                assert got[s] == want[s], s
+                n_dev += 1
+        return n_dev
+
+    def test_format_matches_host(self):
+        rng = np.random.default_rng(5)
+        S, N = 4096, 50
+        # adversarial values (many outside fmt15g's domain -> host): identical wherever formatted
+        vals = codec_corpus.control_values(5, 3000)
+        n_dev = self.format_both(rng.choice(vals, (N, S)), rng.choice(vals, (N, S)),
+                                 rng.integers(0, N + 1, S).astype(np.int32))
+        assert n_dev > 0
+        # trajectories as the planner writes them: every message on the GPU
+        xs = rng.uniform(-3000, 3000, (N, S)) * 10.0 ** rng.integers(-3, 4, (N, S))
+        xs[::7] = np.round(xs[::7])
+        xs[::11] = np.nan
+        ys = rng.uniform(-3000, 3000, (N, S))
+        assert self.format_both(xs, ys, rng.integers(0, N + 1, S).astype(np.int32)) == S

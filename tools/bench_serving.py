@@ -71,6 +71,53 @@ def main():
                             "format_us": t["format"] / a.reps * 1e6, "threads": a.threads,
                             "bytes_in_per_frame": sum(map(len, msgs)) / B,
                             "bytes_out_per_frame": sum(map(len, out)) / B})
+    # the same frames through the GPU codec: bytes H2D -> device parse -> pp_eval on the device batch
+    # -> device format -> slots D2H (frames the device hands back are re-done by the host codec)
+    import torch
+    dev = torch.device("cuda", 0)
+    res["rows_device_codec"] = []
+    for B in [int(b) for b in a.batches.split(",")]:
+        msgs = frames[:B]
+        buf, off = ppamd.pack_messages(msgs)
+        npad = (len(buf) + 15) // 16 * 16 + 16
+        hbuf = torch.zeros(npad, dtype=torch.uint8).pin_memory()
+        hbuf[:len(buf)] = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+        hoff = torch.from_numpy(off).pin_memory()
+        dbuf = torch.empty(npad, dtype=torch.uint8, device=dev)
+        doff = torch.empty(len(off), dtype=torch.int64, device=dev)
+        r = ppamd.alloc_result(B, prm, xp="torch", device=dev)
+        slot = 2560
+        hslots = torch.empty((B, slot), dtype=torch.uint8).pin_memory()
+        hlen = torch.empty(B, dtype=torch.int32).pin_memory()
+
+        def run():
+            dbuf.copy_(hbuf, non_blocking=True)
+            doff.copy_(hoff, non_blocking=True)
+            d, st = ppamd.telemetry_parse_device(None, car_stride=16, d_buf=dbuf, d_off=doff,
+                                                 stream=torch.cuda.current_stream(dev).cuda_stream)
+            ppamd.evaluate(m, d, prm, r, device=0, stream=torch.cuda.current_stream(dev).cuda_stream)
+            slots, ln = ppamd.control_format_device(r["next_x"], r["next_y"], r["n_out"], slot_bytes=slot,
+                                                    stream=torch.cuda.current_stream(dev).cuda_stream)
+            hslots.copy_(slots, non_blocking=True)
+            hlen.copy_(ln, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            return st
+        st = run()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            st = run()
+        t1 = time.perf_counter()
+        msgs_out = ppamd.slots_to_messages(hslots.numpy(), hlen.numpy())
+        n_host = int((st.cpu().numpy() == ppamd.MSG_HOST).sum()) + sum(m_ is None for m_ in msgs_out)
+        # spot check: identical bytes to the host codec path
+        hd, _ = ppamd.telemetry_parse(msgs[:256], threads=a.threads)
+        hr = ppamd.plan_batch_host(m, hd, prm)
+        same = ppamd.control_format(hr["next_x"], hr["next_y"], hr["n_out"])
+        agree = sum(int(msgs_out[i] == same[i]) for i in range(min(256, B)))
+        tot = (t1 - t0) / a.reps
+        res["rows_device_codec"].append({"batch": B, "frames_per_s": B / tot, "us_per_batch": tot * 1e6,
+                                         "frames_for_host_codec": n_host, "bytes_h2d": npad, "bytes_d2h": B * slot,
+                                         "first_256_identical_to_host_path": agree})
     # the reference's per-frame path on one core
     import oracle_lib
     rj, rlib = oracle_lib.load_ref_json(), oracle_lib.load_ref()
