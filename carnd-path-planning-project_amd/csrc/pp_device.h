@@ -96,6 +96,10 @@ __device__ inline void init_reference_waypoint(const MapV& m, double x, double y
 }
 
 // Map::lane_matching (src/main.cpp:199-275); bounded walk (never reached on finite input).
+// The reference computes s, d, lane and next_wp at every improvement (:214-227); only the last
+// improvement's values survive, so the walk records that projection's raw terms (lane, segment,
+// rnom, rdenom, snom, the lane's running sum_s and ratio shift) and evaluates the same
+// expressions once after the walk: identical results, one division and one sqrt per walk.
 __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double ratio[3], double x,
                                      double y, double& out_s, double& out_d, int& out_lane,
                                      int& out_next_wp) {
@@ -107,6 +111,8 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
     double sr0 = ratio[0], sr1 = ratio[1], sr2 = ratio[2];
     double best = 1000 * 1000;
     bool found = false;
+    int b_lane = 0, b_cur = 0;
+    double b_rnom = 0, b_rdenom = 1, b_snom = 0, b_ss = 0, b_sr = 0;
     for (int it = 0; it < 4 * n + 8; it++) {
         bool improved = false;
         const int a = wpi(cur - 1, n), b = wpi(cur, n);
@@ -120,17 +126,11 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
                 best = dsq;
                 improved = true;
                 found = true;
-                const double sr = lane == 0 ? sr0 : (lane == 1 ? sr1 : sr2);
-                const double ss = lane == 0 ? sum_s0 : (lane == 1 ? sum_s1 : sum_s2);
-                const double rfs = rnom / rdenom;
-                const double r_mod = rfs - sr;
-                const double seg_len = m.llen[lane * n + b];
-                out_s = ss + seg_len * r_mod;
-                double d = sqrt(dsq);
-                if (snom < 0) d = -d;
-                out_d = d + lane_offset(lane);
-                out_lane = lane;
-                out_next_wp = cur;
+                b_lane = lane;
+                b_cur = cur;
+                b_rnom = rnom; b_rdenom = rdenom; b_snom = snom;
+                b_sr = lane == 0 ? sr0 : (lane == 1 ? sr1 : sr2);
+                b_ss = lane == 0 ? sum_s0 : (lane == 1 ? sum_s1 : sum_s2);
             }
             if (rnom == 0) {
                 if (dir == 1) stop = true;
@@ -153,6 +153,17 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
             sr0 = sr1 = sr2 = 1;
             cur--;
         }
+    }
+    if (found) {                                                   // :214-227, last improvement
+        const double rfs = b_rnom / b_rdenom;
+        const double r_mod = rfs - b_sr;
+        const double seg_len = m.llen[b_lane * n + wpi(b_cur, n)];
+        out_s = b_ss + seg_len * r_mod;
+        double d = sqrt(best);
+        if (b_snom < 0) d = -d;
+        out_d = d + lane_offset(b_lane);
+        out_lane = b_lane;
+        out_next_wp = b_cur;
     }
     return found;
 }

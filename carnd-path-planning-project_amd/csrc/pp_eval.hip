@@ -48,7 +48,10 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
     return m;
 }
 
-__global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+#ifndef PP_PREP_WAVES
+#define PP_PREP_WAVES 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
@@ -123,7 +126,11 @@ __global__ __launch_bounds__(256) void k_prep(MapG mg, pp_scene_batch in, pp_par
     // (re-matched; slot overwritten, or erased when matching fails, src/main.cpp:1329-1348) or
     // taken from its stale slot.
     const bool tab = in.tab_valid != nullptr;
+#ifdef PP_ABL_PREP_NOCARS   // diagnostic timing build: ego only
+    const int iters = 0;
+#else
     const int iters = tab ? PP_MAX_CARS : ncar;
+#endif
     int p = 0;                              // next unread row (table mode)
     for (int it = 0; it < iters; it++) {
         int row = it;
