@@ -191,6 +191,48 @@ __device__ inline void project_speed(const MapV& m, double vx, double vy, int ne
     vd = (snom / rdenom) * svl * sign;
 }
 
+// get_lane_pos for K increasing positive targets s[0..K) in one forward walk. Every call with
+// s > 0 walks forward only (s stays > 0 until s <= remaining_length, :291-302), through the same
+// segments with the same remaining lengths, so target i sees exactly its own call's sequence of
+// subtractions and stops where that call stops: identical points and ok flags.
+template <int K>
+__device__ inline void get_lane_pos_multi(const MapV& m, int ref_wp, double ratio, const double* s_in, int lane,
+                                          double* ox, double* oy, bool* ok) {
+    const int n = m.n;
+    double sv[K];
+    unsigned pending = (1u << K) - 1;
+#pragma unroll
+    for (int i = 0; i < K; i++) { sv[i] = s_in[i]; ok[i] = false; ox[i] = 0; oy[i] = 0; }
+    int wp = ref_wp;
+    double nx_ = 0, ny_ = 0, px_ = 0, py_ = 0;
+    for (int it = 0; it < 4 * n + 8 && pending; it++) {
+        const int b = wpi(wp, n), a = wpi(wp - 1, n);
+        nx_ = m.lc_x[lane * n + b]; ny_ = m.lc_y[lane * n + b];
+        px_ = m.lc_x[lane * n + a]; py_ = m.lc_y[lane * n + a];
+        const double wl = m.llen[lane * n + b];
+        const double rem = wl * (1 - ratio);
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            if (!((pending >> i) & 1)) continue;
+            if (sv[i] <= rem) {
+                const double dest = 1 - (rem - sv[i]) / wl;
+                ox[i] = nx_ * dest + px_ * (1 - dest);
+                oy[i] = ny_ * dest + py_ * (1 - dest);
+                ok[i] = true;
+                pending &= ~(1u << i);
+            } else {
+                sv[i] -= rem;
+            }
+        }
+        ratio = 0;
+        wp++;
+    }
+    // a target the bounded walk did not reach: its call ends on the last segment with dest 0
+#pragma unroll
+    for (int i = 0; i < K; i++)
+        if ((pending >> i) & 1) { ox[i] = nx_ * 0.0 + px_ * (1 - 0.0); oy[i] = ny_ * 0.0 + py_ * (1 - 0.0); }
+}
+
 // Map::get_lane_pos (src/main.cpp:277-328) on one lane. ok=false if the bounded walk ran out.
 __device__ inline void get_lane_pos(const MapV& m, int ref_wp, double ratio, double s, int lane,
                                     double& ox, double& oy, bool& ok) {

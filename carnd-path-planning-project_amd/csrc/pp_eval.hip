@@ -371,12 +371,20 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
     sl.x(npk) = (pos_x - pos_x) * ca - (pos_y - pos_y) * sa;
     sl.y(npk) = (pos_x - pos_x) * sa + (pos_y - pos_y) * ca;
     int ncp = 1;
-    double cps = dist;
+    // the five candidate control points (:744-768); their lane positions in one walk when the
+    // targets are positive (always, unless the telemetry speed is not finite)
+    double cpsv[5], cpx[5], cpy[5];
+    bool cok[5];
+    cpsv[0] = dist;
+    for (int i = 1; i < 5; i++) cpsv[i] = cpsv[i - 1] + min_cpd;
+    if (cpsv[0] > 0 && cpsv[1] > 0 && cpsv[2] > 0 && cpsv[3] > 0 && cpsv[4] > 0) {
+        get_lane_pos_multi<5>(m, ref_wp, ratio, cpsv, L, cpx, cpy, cok);
+    } else {
+        for (int i = 0; i < 5; i++) get_lane_pos(m, ref_wp, ratio, cpsv[i], L, cpx[i], cpy[i], cok[i]);
+    }
     for (int i = 0; i < 5; i++) {
-        double npx, npy;
-        bool ok;
-        get_lane_pos(m, ref_wp, ratio, cps, L, npx, npy, ok);
-        if (!ok) flags |= kMetaWalkFail;
+        const double npx = cpx[i], npy = cpy[i];
+        if (!cok[i]) flags |= kMetaWalkFail;
         total += sqrt((npx - lx) * (npx - lx) + (npy - ly) * (npy - ly));
         lx = npx; ly = npy;
         const double tx0 = npx - pos_x, ty0 = npy - pos_y;
@@ -384,7 +392,6 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
         sl.y(npk + ncp) = tx0 * sa + ty0 * ca;
         ncp++;
         if (total > 50 && ncp > 2) break;
-        cps += min_cpd;
     }
     int nk = npk + ncp;
     for (int i = 1; i < nk; i++) {                                      // :833-843
