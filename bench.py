@@ -49,6 +49,26 @@ def max_over_ranks(elapsed, dist, device):
     return float(t.item())
 
 
+def load_valu_peak():
+    """Measured FP64 VALU issue rate (tools/valu_peak.hip on the MI355X, profiles/r01_valu_peak.json)."""
+    p = os.path.join(REPO, "profiles", "r01_valu_peak.json")
+    try:
+        return json.load(open(p))["v_fma_f64"]["wave_instr_per_s"]
+    except Exception:
+        return None
+
+
+def load_f64_instr(tag):
+    """FP64 VALU wave-instructions per k_cand launch from the committed PMC summary."""
+    p = os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        c = json.load(open(p))[tag]["counters"]
+        return sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")), c.get("SQ_INSTS_VALU")
+    except Exception:
+        return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,6 +232,17 @@ def main():
                      "kernel": "k_cand", "algorithmic_bytes_per_candidate": bpc,
                      "traffic_source": traffic_src},
     }
+    # the bound that matters for this path: FP64 VALU issue (no MFMA-shaped work, HBM ~3 %)
+    f64, allv = load_f64_instr(tag)
+    peak = load_valu_peak()
+    if f64 and peak:
+        ach = f64 / (k_cand_ms * 1e-3)
+        out["valu_roofline"] = {"bound": "fp64-valu-issue", "kernel": "k_cand",
+                                "achieved_f64_wave_instr_per_s": ach, "peak_f64_fma_wave_instr_per_s": peak,
+                                "frac": ach / peak, "all_valu_wave_instr_per_launch": allv,
+                                "f64_wave_instr_per_launch": f64,
+                                "source": "rocprofv3 PMC SQ_INSTS_VALU_*_F64 per launch (profiles/pmc_summary.json) "
+                                          "/ this run's k_cand time; peak measured by tools/valu_peak.hip"}
     if a.rollout:
         out["scene_frames_per_s"] = S * world * a.steps * frames / elapsed
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
