@@ -14,7 +14,9 @@ __global__ __launch_bounds__(256) void k_chain(double* out, int iters, double s)
         else if (kOp == 1) x = x * s;                                  \
         else if (kOp == 2) x = x + s;                                  \
         else if (kOp == 3) x = __builtin_amdgcn_rcp(x + s);           \
-        else x = __builtin_sqrt(x + s);
+        else if (kOp == 4) x = __builtin_sqrt(x + s);                  \
+        else if (kOp == 5) x = s / (x + 0.5);                          \
+        else x = __builtin_fma(__builtin_fma(-(x + 0.5), __builtin_amdgcn_rcp(x + 0.5), 1.0), s, x);
         STEP(a0) STEP(a1) STEP(a2) STEP(a3) STEP(a4) STEP(a5) STEP(a6) STEP(a7)
     }
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
@@ -42,12 +44,14 @@ int main() {
     const int iters = 20000;
     double* d;
     hipMalloc(&d, sizeof(double) * blocks * 256);
-    const char* names[5] = {"v_fma_f64", "v_mul_f64", "v_add_f64", "v_rcp_f64(+add)", "sqrt_f64(+add)"};
-    double secs[5] = {run<0>(d, blocks, iters, 0.999999), run<1>(d, blocks, iters, 0.999999),
-                      run<2>(d, blocks, iters, 1e-9), run<3>(d, blocks, iters, 0.5), run<4>(d, blocks, iters, 0.5)};
+    const char* names[7] = {"v_fma_f64", "v_mul_f64", "v_add_f64", "v_rcp_f64(+add)", "sqrt_f64(+add)",
+                            "ieee_div_f64(+add)", "rcp+2fma(+2add)"};
+    double secs[7] = {run<0>(d, blocks, iters, 0.999999), run<1>(d, blocks, iters, 0.999999),
+                      run<2>(d, blocks, iters, 1e-9), run<3>(d, blocks, iters, 0.5), run<4>(d, blocks, iters, 0.5),
+                      run<5>(d, blocks, iters, 0.7), run<6>(d, blocks, iters, 0.7)};
     const double waves = blocks * 4.0;
     printf("{\"cus\": %d, \"clock_mhz\": %d", cus, p.clockRate / 1000);
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < 7; k++) {
         const double winstr = waves * iters * 8.0;          // wave-instructions of the op (k >= 3: op + add)
         printf(", \"%s\": {\"wave_instr_per_s\": %.4e, \"lane_ops_per_s\": %.4e}", names[k], winstr / secs[k],
                winstr * 64 / secs[k]);
