@@ -51,13 +51,19 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #ifndef PP_PREP_WAVES
 #define PP_PREP_WAVES 3
 #endif
+// kLdsMap: the map (13 n doubles) is staged in LDS (n <= kLdsMapMax); larger maps are read from
+// global memory (L2-resident) by the same code.
+constexpr int kLdsMapMax = 600;
+template <bool kLdsMap>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
-    for (int i = threadIdx.x; i < 13 * n; i += blockDim.x) smap[i] = mg.buf[i];
-    __syncthreads();
-    const MapV m = map_view(smap, n);
+    if (kLdsMap) {
+        for (int i = threadIdx.x; i < 13 * n; i += blockDim.x) smap[i] = mg.buf[i];
+        __syncthreads();
+    }
+    const MapV m = map_view(kLdsMap ? smap : mg.buf, n);
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
@@ -1010,6 +1016,62 @@ __global__ __launch_bounds__(256) void k_synth_traffic(ppsynth::LaneTables T, ui
 }
 
 // ------------------------------------------------------------------------------------------------
+// Map::Init on the device (src/main.cpp:89-131; pp_map_create_device). g: the MapG layout
+// (13 n: ref x/y, normal x/y, lane centres x[3]/y[3], lane lengths[3]); t: the synth lane tables
+// (15 n). Three passes because each reads its neighbours' results of the previous one.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wrap_i(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
+
+__global__ __launch_bounds__(256) void k_map_normals(const double* wx, const double* wy, int n, double* g,
+                                                     int* bad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int p = wrap_i(i - 1, n);
+    const double dx = wx[i] - wx[p], dy = wy[i] - wy[p];
+    const double len = sqrt(dx * dx + dy * dy);
+    if (!(len > 0)) atomicOr(bad, 1);                 // duplicate consecutive waypoints
+    g[i] = wx[i]; g[n + i] = wy[i];
+    g[2 * n + i] = dy / len;
+    g[3 * n + i] = -dx / len;
+}
+
+__global__ __launch_bounds__(256) void k_map_lanes(int n, double* g) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int q = wrap_i(i + 1, n);
+    const double nx = g[2 * n + i], ny = g[3 * n + i];
+    double ax = (nx + g[2 * n + q]) / 2, ay = (ny + g[3 * n + q]) / 2;
+    const double a_n = ppm::atan2_pp(ny, nx);
+    const double a_avg = ppm::atan2_pp(ay, ax);
+    double s_, c_;
+    ppm::sincos_pp<true>(a_avg - a_n, s_, c_);
+    ax /= c_;
+    ay /= c_;
+    for (int r = 0; r < 3; r++) {
+        const double off = 4.0 * (r + 0.5);
+        g[(4 + r) * n + i] = g[i] + ax * off;
+        g[(7 + r) * n + i] = g[n + i] + ay * off;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_map_lengths(int n, double* g, double* t) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int p = wrap_i(i - 1, n);
+    for (int r = 0; r < 3; r++) {
+        const double lx = g[(4 + r) * n + i], ly = g[(7 + r) * n + i];
+        const double dx = lx - g[(4 + r) * n + p], dy = ly - g[(7 + r) * n + p];
+        const double len = sqrt(dx * dx + dy * dy);
+        g[(10 + r) * n + i] = len;                                   // Map::get_lane_length
+        t[0 * 3 * n + r * n + i] = lx;
+        t[1 * 3 * n + r * n + i] = ly;
+        t[2 * 3 * n + r * n + i] = len;
+        t[3 * 3 * n + r * n + i] = dx / len;
+        t[4 * 3 * n + r * n + i] = dy / len;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // scene synthesis
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_synth(ppsynth::LaneTables T, uint64_t seed, int64_t first,
@@ -1025,6 +1087,7 @@ __global__ __launch_bounds__(256) void k_synth(ppsynth::LaneTables T, uint64_t s
 namespace {
 
 constexpr int kMaxDev = 16;
+constexpr int kMaxWaypoints = 1 << 24;
 constexpr int kPrepD = 7 + 3 + 2 + 3 + 9 + 3;   // doubles per scene in PrepV (see prep_bind)
 constexpr int kPrepI = 7;
 
@@ -1269,11 +1332,65 @@ double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int3
 const char* pp_version(void) { return "pp-mi355x 0.1 (gfx950, fp64, lane-per-candidate)"; }
 
 int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out) {
-    if (!wx || !wy || !out || n < 3 || n > 600) return PP_ERR_ARG;   // map staged in LDS: 13 * n doubles <= 64 KB
+    if (!wx || !wy || !out || n < 3 || n > kMaxWaypoints) return PP_ERR_ARG;
     pp_map* M = new (std::nothrow) pp_map();
     if (!M) return PP_ERR_NOMEM;
     const int rc = build_map(M, wx, wy, n);
     if (rc != PP_OK) { delete M; return rc; }
+    *out = M;
+    return PP_OK;
+}
+
+// Map::Init on the device from device waypoint arrays; the derived tables are mirrored to the host
+// (for pp_map_geometry, the host generator and other devices).
+int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, int32_t device, void* hip_stream,
+                             pp_map** out) {
+    if (!d_wx || !d_wy || !out || n < 3 || n > kMaxWaypoints || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
+    pp_map* M = new (std::nothrow) pp_map();
+    if (!M) return PP_ERR_NOMEM;
+    M->n = n;
+    DeviceGuard g(device);
+    DevState& D = M->dev[device];
+    hipStream_t st = (hipStream_t)hip_stream;
+    int* bad = nullptr;
+    if (hipMalloc(&D.map, sizeof(double) * 13 * (size_t)n) != hipSuccess ||
+        hipMalloc(&D.lanetab, sizeof(double) * 15 * (size_t)n) != hipSuccess || hipMalloc(&bad, sizeof(int)) != hipSuccess) {
+        if (D.map) (void)hipFree(D.map);
+        if (D.lanetab) (void)hipFree(D.lanetab);
+        delete M;
+        return PP_ERR_NOMEM;
+    }
+    int rc = PP_OK;
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (hipMemsetAsync(bad, 0, sizeof(int), st) != hipSuccess) rc = PP_ERR_HIP;
+    hipLaunchKernelGGL(k_map_normals, dim3(blocks), dim3(256), 0, st, d_wx, d_wy, n, D.map, bad);
+    hipLaunchKernelGGL(k_map_lanes, dim3(blocks), dim3(256), 0, st, n, D.map);
+    hipLaunchKernelGGL(k_map_lengths, dim3(blocks), dim3(256), 0, st, n, D.map, D.lanetab);
+    if (hipGetLastError() != hipSuccess) rc = PP_ERR_HIP;
+    int hbad = 0;
+    M->geom.assign(13 * (size_t)n, 0.0);
+    M->lanetab.assign(15 * (size_t)n, 0.0);
+    if (rc == PP_OK && (hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(M->geom.data(), D.map, sizeof(double) * 13 * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(M->lanetab.data(), D.lanetab, sizeof(double) * 15 * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess))
+        rc = PP_ERR_HIP;
+    (void)hipFree(bad);
+    if (rc == PP_OK && hbad) rc = PP_ERR_ARG;          // Map::Init divides by a zero segment length
+    if (rc != PP_OK) {
+        (void)hipFree(D.map); (void)hipFree(D.lanetab);
+        D.map = D.lanetab = nullptr;
+        delete M;
+        return rc;
+    }
+    const double* gg = M->geom.data();
+    M->ptab.assign(10 * (size_t)n, 0.0);
+    for (int i = 0; i < n; i++) {
+        double* o = &M->ptab[10 * (size_t)i];
+        o[0] = gg[i]; o[1] = gg[n + i]; o[2] = gg[2 * n + i]; o[3] = gg[3 * n + i];
+        for (int r = 0; r < 3; r++) { o[4 + 2 * r] = gg[(4 + r) * n + i]; o[5 + 2 * r] = gg[(7 + r) * n + i]; }
+    }
+    D.init = true;
     *out = M;
     return PP_OK;
 }
@@ -1385,9 +1502,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     {
         const int threads = 256;
         const int64_t blocks = (Sv + threads - 1) / threads;
-        const size_t lds = sizeof(double) * 13 * (size_t)mg.n;
         if (timing) (void)hipEventRecord(ev[0], st);
-        hipLaunchKernelGGL(k_prep, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status);
+        if (mg.n <= kLdsMapMax) {
+            const size_t lds = sizeof(double) * 13 * (size_t)mg.n;
+            hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status);
+        } else {
+            hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status);
+        }
     }
     // K2
     {

@@ -117,7 +117,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
-           "pp_telemetry_parse_device", "pp_control_format_device"]
+           "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device"]
 
 
 def _load():
@@ -138,6 +138,9 @@ def _load():
     lib.pp_version.restype = C.c_char_p
     lib.pp_map_create.argtypes = [_dp, _dp, C.c_int32, C.POINTER(C.c_void_p)]
     lib.pp_map_create.restype = C.c_int32
+    lib.pp_map_create_device.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                         C.POINTER(C.c_void_p)]
+    lib.pp_map_create_device.restype = C.c_int32
     lib.pp_map_destroy.argtypes = [C.c_void_p]
     lib.pp_map_destroy.restype = C.c_int32
     lib.pp_map_geometry.argtypes = [C.c_void_p, _dp, C.c_int32]
@@ -249,6 +252,19 @@ class Map:
         _check(lib.pp_map_create(self.wx.ctypes.data_as(_dp), self.wy.ctypes.data_as(_dp),
                                  self.n, C.byref(h)), "pp_map_create")
         self.handle = h
+
+    @classmethod
+    def from_device(cls, d_wx, d_wy, device=0, stream=None):
+        """pp_map_create_device: Map::Init on the GPU from torch waypoint tensors."""
+        self = cls.__new__(cls)
+        self.wx = d_wx.detach().cpu().numpy().astype(np.float64)
+        self.wy = d_wy.detach().cpu().numpy().astype(np.float64)
+        self.n = len(self.wx)
+        h = C.c_void_p()
+        _check(lib.pp_map_create_device(d_wx.data_ptr(), d_wy.data_ptr(), self.n, device, stream, C.byref(h)),
+               "pp_map_create_device")
+        self.handle = h
+        return self
 
     def geometry(self) -> np.ndarray:
         out = np.zeros((self.n, 10), np.float64)

@@ -179,8 +179,15 @@ typedef struct pp_map pp_map;
 void    pp_params_default(pp_params* p);
 int32_t pp_num_candidates(const pp_params* p);
 
-/* Map::Init (src/main.cpp:89-131) on the host; the lane geometry is uploaded lazily per device. */
+/* Map::Init (src/main.cpp:89-131) on the host (bit-identical to the reference's); the lane
+ * geometry is uploaded lazily per device. n >= 3 waypoints, any size. */
 int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out);
+/* Map::Init on `device` from DEVICE waypoint arrays: the same formulas
+ * with the device's atan2/cos (the reference's lane centres within ~1e-12 m instead of bit for
+ * bit); tables mirrored to the host. Maps of any size (> 600 waypoints: the planner reads the map
+ * from global memory instead of staging it in LDS). Synchronous on hip_stream. */
+int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, int32_t device, void* hip_stream,
+                             pp_map** out);
 int32_t pp_map_destroy(pp_map* m);
 /* host copy of the derived geometry: per waypoint {ref.x, ref.y, nx, ny, lc0.x, lc0.y, lc1.x,
  * lc1.y, lc2.x, lc2.y} (10 doubles) — the Map::Init known-answer output. */
