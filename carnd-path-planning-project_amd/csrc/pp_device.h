@@ -15,6 +15,8 @@ namespace ppd {
 constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
 constexpr double kEps = 1e-5;                     // src/main.cpp:24
 constexpr int kKP = 17;                           // LDS knot stride (16 knots + 1 pad: bank spread)
+constexpr int NL = PP_NUM_LANES;                  // lanes (src/main.cpp:22)
+constexpr int kMapArrays = 4 + 3 * NL;            // ref x/y, normal x/y, lane centre x[NL]/y[NL], length[NL]
 
 // Map geometry (SoA). Arrays [i] or [lane * n + i]. llen[lane*n+i] = |lc[i] - lc[i-1]|
 // (Map::get_lane_length, src/main.cpp:138-142), precomputed on the host with the same formula.
@@ -26,8 +28,8 @@ struct MapV {
 // Per-scene preparation output of K1 (SoA, workspace).
 struct PrepV {
     double *pos_x, *pos_y, *angle, *ca_m, *sa_m, *ca_p, *sa_p;
-    double *ego_speed, *ego_d, *ego_vd, *ratio /*[3][S]*/, *in_ts, *in_tt, *l_ts /*[3][S]*/,
-        *l_tt /*[3][S]*/, *score /*[3][S]*/;
+    double *ego_speed, *ego_d, *ego_vd, *ratio /*[NL][S]*/, *in_ts, *in_tt, *l_ts /*[NL][S]*/,
+        *l_tt /*[NL][S]*/, *score /*[NL][S]*/;
     int32_t *K, *ref_wp, *T, *ego_lane, *open_mask, *lim_mask, *status;
 };
 
@@ -62,7 +64,7 @@ __device__ __forceinline__ double distsq_pt_seg(double px, double py, double ax,
 
 // Map::init_reference_waypoint (src/main.cpp:143-197)
 __device__ inline void init_reference_waypoint(const MapV& m, double x, double y, int& ref_wp,
-                                               double ratio[3]) {
+                                               double ratio[NL]) {
     const int n = m.n;
     int closest = 0;
     double cd;
@@ -88,7 +90,7 @@ __device__ inline void init_reference_waypoint(const MapV& m, double x, double y
     }
     ref_wp = closest;
     const int a = wpi(closest - 1, n), b = wpi(closest, n);
-    for (int lane = 0; lane < 3; lane++) {
+    for (int lane = 0; lane < NL; lane++) {
         distsq_pt_seg(x, y, m.lc_x[lane * n + a], m.lc_y[lane * n + a], m.lc_x[lane * n + b],
                       m.lc_y[lane * n + b], rnom, rdenom, snom);
         ratio[lane] = rnom / rdenom;
@@ -100,15 +102,16 @@ __device__ inline void init_reference_waypoint(const MapV& m, double x, double y
 // improvement's values survive, so the walk records that projection's raw terms (lane, segment,
 // rnom, rdenom, snom, the lane's running sum_s and ratio shift) and evaluates the same
 // expressions once after the walk: identical results, one division and one sqrt per walk.
-__device__ inline bool lane_matching(const MapV& m, int ref_wp, const double ratio[3], double x,
+__device__ inline bool lane_matching(const MapV& m, int ref_wp, const double ratio[NL], double x,
                                      double y, double& out_s, double& out_d, int& out_lane,
                                      int& out_next_wp) {
     const int n = m.n;
     int dir = 0;
     bool stop = false;
     int cur = ref_wp;
-    double sum_s0 = 0, sum_s1 = 0, sum_s2 = 0;
-    double sr0 = ratio[0], sr1 = ratio[1], sr2 = ratio[2];
+    double sum_s[NL], sr[NL];
+#pragma unroll
+    for (int l = 0; l < NL; l++) { sum_s[l] = 0; sr[l] = ratio[l]; }
     double best = 1000 * 1000;
     bool found = false;
     int b_lane = 0, b_cur = 0;
@@ -117,7 +120,7 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
         bool improved = false;
         const int a = wpi(cur - 1, n), b = wpi(cur, n);
 #pragma unroll
-        for (int lane = 0; lane < 3; lane++) {
+        for (int lane = 0; lane < NL; lane++) {
             double rnom, snom, rdenom;
             const double dsq = distsq_pt_seg(x, y, m.lc_x[lane * n + a], m.lc_y[lane * n + a],
                                              m.lc_x[lane * n + b], m.lc_y[lane * n + b], rnom,
@@ -129,8 +132,8 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
                 b_lane = lane;
                 b_cur = cur;
                 b_rnom = rnom; b_rdenom = rdenom; b_snom = snom;
-                b_sr = lane == 0 ? sr0 : (lane == 1 ? sr1 : sr2);
-                b_ss = lane == 0 ? sum_s0 : (lane == 1 ? sum_s1 : sum_s2);
+                b_sr = sr[lane];
+                b_ss = sum_s[lane];
             }
             if (rnom == 0) {
                 if (dir == 1) stop = true;
@@ -143,14 +146,16 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
             }
         }
         if (!improved || stop) break;
-        const double l0 = m.llen[0 * n + b], l1 = m.llen[1 * n + b], l2 = m.llen[2 * n + b];
+        double ll[NL];
+#pragma unroll
+        for (int l = 0; l < NL; l++) ll[l] = m.llen[l * n + b];
         if (dir > 0) {
-            sum_s0 += (1 - sr0) * l0; sum_s1 += (1 - sr1) * l1; sum_s2 += (1 - sr2) * l2;
-            sr0 = sr1 = sr2 = 0;
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] += (1 - sr[l]) * ll[l]; sr[l] = 0; }
             cur++;
         } else {
-            sum_s0 -= sr0 * l0; sum_s1 -= sr1 * l1; sum_s2 -= sr2 * l2;
-            sr0 = sr1 = sr2 = 1;
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] -= sr[l] * ll[l]; sr[l] = 1; }
             cur--;
         }
     }

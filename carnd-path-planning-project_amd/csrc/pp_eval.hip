@@ -33,7 +33,7 @@ using namespace ppd;
 // ------------------------------------------------------------------------------------------------
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
-// 13 arrays of n: ref_x ref_y nx ny lc_x[3] lc_y[3] llen[3]
+// kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL]
 struct MapG { const double* buf; int n; };
 
 // |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
@@ -44,23 +44,23 @@ constexpr int kLimSlow = 1 << 7;   // internal bit in PrepV.lim_mask
 __device__ __forceinline__ MapV map_view(const double* b, int n) {
     MapV m;
     m.ref_x = b; m.ref_y = b + n; m.nx = b + 2 * n; m.ny = b + 3 * n;
-    m.lc_x = b + 4 * n; m.lc_y = b + 7 * n; m.llen = b + 10 * n; m.n = n;
+    m.lc_x = b + 4 * n; m.lc_y = b + (4 + NL) * n; m.llen = b + (4 + 2 * NL) * n; m.n = n;
     return m;
 }
 
 #ifndef PP_PREP_WAVES
 #define PP_PREP_WAVES 3
 #endif
-// kLdsMap: the map (13 n doubles) is staged in LDS (n <= kLdsMapMax); larger maps are read from
-// global memory (L2-resident) by the same code.
-constexpr int kLdsMapMax = 600;
+// kLdsMap: the map (kMapArrays n doubles) is staged in LDS (n <= kLdsMapMax: <= 62.4 KB, 600
+// waypoints at three lanes); larger maps are read from global memory (L2-resident) by the same code.
+constexpr int kLdsMapMax = 62400 / (8 * kMapArrays);
 template <bool kLdsMap>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
     if (kLdsMap) {
-        for (int i = threadIdx.x; i < 13 * n; i += blockDim.x) smap[i] = mg.buf[i];
+        for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
         __syncthreads();
     }
     const MapV m = map_view(kLdsMap ? smap : mg.buf, n);
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     }
     // ---- Frenet frame + ego matching (src/main.cpp:1299-1320) ----
     int ref_wp;
-    double ratio[3];
+    double ratio[NL];
     init_reference_waypoint(m, ego_x, ego_y, ref_wp, ratio);
     double ego_s = 0, ego_d = 0;
     int ego_lane = 0, nwp_unused = 0;
@@ -118,12 +118,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // LaneChangePlanner accumulation (src/main.cpp:377-445) and follow-car selection
     // (src/main.cpp:1388-1410) are order-dependent reductions over the same car sequence.
     const int T_in = in.prev_target_lane[s];
-    double lane_speed[3] = {P.max_speed, P.max_speed, P.max_speed};
-    double next_s[3] = {1000, 1000, 1000};
-    bool open[3] = {true, true, true};
+    double lane_speed[NL], next_s[NL];
+    bool open[NL];
     int in_id = -1; double in_s = 0, in_vx = 0, in_vy = 0;
-    int t_id[3] = {-1, -1, -1};
-    double t_s[3] = {0, 0, 0}, t_vx[3] = {0, 0, 0}, t_vy[3] = {0, 0, 0};
+    int t_id[NL];
+    double t_s[NL], t_vx[NL], t_vy[NL];
+#pragma unroll
+    for (int l = 0; l < NL; l++) {
+        lane_speed[l] = P.max_speed; next_s[l] = 1000; open[l] = true;
+        t_id[l] = -1; t_s[l] = 0; t_vx[l] = 0; t_vy[l] = 0;
+    }
     int nmatched = 0;
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             if (in_id == -1 || in_s > s0) { in_id = id; in_s = s0; in_vx = cvx; in_vy = cvy; }
         }
 #pragma unroll
-        for (int L = 0; L < 3; L++) {
+        for (int L = 0; L < NL; L++) {
             if (s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3) {
                 if (t_id[L] == -1 || t_s[L] > s0) { t_id[L] = id; t_s[L] = s0; t_vx[L] = cvx; t_vy[L] = cvy; }
             }
@@ -228,9 +232,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // scores + argmax (src/main.cpp:447-484)
     int best_lane = ego_lane;
     double best_score = 0;
-    double score[3];
+    double score[NL];
 #pragma unroll
-    for (int lane = 0; lane < 3; lane++) {
+    for (int lane = 0; lane < NL; lane++) {
         score[lane] = 0;
         if (lane != ego_lane && !open[lane]) continue;
         const double speed_score = s_min(lane_speed[lane] / P.max_speed, 1.0);
@@ -248,8 +252,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     } else {
         T = best_lane;
     }
-    const int open_mask = (open[0] ? 1 : 0) | (open[1] ? 2 : 0) | (open[2] ? 4 : 0);
-    if (open_mask != 7) status |= PP_ST_LANE_CLOSED;
+    int open_mask = 0;
+#pragma unroll
+    for (int l = 0; l < NL; l++) open_mask |= open[l] ? (1 << l) : 0;
+    if (open_mask != (1 << NL) - 1) status |= PP_ST_LANE_CLOSED;
     if (T != ego_lane) {                                               // src/main.cpp:1358-1369
         const double dtl = lane_offset(T);
         const double diff = fabs(ego_vd * 1.0 + ego_d - dtl);
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         lim_mask |= 1;
     }
 #pragma unroll
-    for (int L = 0; L < 3; L++) {
+    for (int L = 0; L < NL; L++) {
         if (t_id[L] >= 0 && t_id[L] != in_id) {
             double ts, tt;
             const int code = limit_speed(P, t_vx[L], t_vy[L], t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     pv.ca_p[v] = cp; pv.sa_p[v] = sp_;
     pv.ego_speed[v] = ego_speed; pv.ego_d[v] = ego_d; pv.ego_vd[v] = ego_vd;
 #pragma unroll
-    for (int l = 0; l < 3; l++) { pv.ratio[l * Sv + v] = ratio[l]; pv.score[l * Sv + v] = score[l]; }
+    for (int l = 0; l < NL; l++) { pv.ratio[l * Sv + v] = ratio[l]; pv.score[l * Sv + v] = score[l]; }
     pv.K[v] = K; pv.ref_wp[v] = ref_wp; pv.T[v] = T; pv.ego_lane[v] = ego_lane;
     pv.open_mask[v] = open_mask; pv.lim_mask[v] = lim_mask; pv.status[v] = status;
     if (draw == 0) out_status[s] = 0;        // k_cand ORs its flags in (atomics when a scene spans blocks)
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         pp_scene_info I = {};
         I.ego_x = ego_x; I.ego_y = ego_y; I.ego_speed = ego_speed; I.ego_acc = ego_acc;
         I.ego_s = ego_s; I.ego_d = ego_d; I.ego_vs = ego_vs; I.ego_vd = ego_vd;
-        for (int l = 0; l < 3; l++) { I.ref_ratio[l] = ratio[l]; I.lane_score[l] = score[l]; }
+        for (int l = 0; l < NL; l++) { I.ref_ratio[l] = ratio[l]; I.lane_score[l] = score[l]; }
         I.ref_wp = ref_wp; I.ego_lane = ego_lane; I.target_lane = T; I.lane_open_mask = open_mask;
         I.n_matched_cars = nmatched; I.in_lane_car = in_id;
         info[s] = I;
@@ -677,10 +683,10 @@ template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int NS = P.n_speeds, Cv = 3 * NS, N = P.n_points;
+    const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int C = D * Cv;                     // candidates per scene (all draws)
-    const int nslot = 3 * SPB;
+    const int nslot = NL * SPB;
     double* sX = sm;
     double* sY = sX + nslot * kKP;
     double* sA = sY + nslot * kKP;
@@ -704,10 +710,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         if (!__syncthreads_or(mine)) return;
     }
     if (tid < SPB) sFlags[tid] = 0;
-    if (tid < 3 * nsc && (((pv.lim_mask[(s0 + tid / 3) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
+    if (tid < NL * nsc && (((pv.lim_mask[(s0 + tid / NL) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
         const int j = tid;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
-        setup_lane(m, P, in, pv, s0 + j / 3, (s0 + j / 3) * D, Sv, j % 3, sl);
+        setup_lane(m, P, in, pv, s0 + j / NL, (s0 + j / NL) * D, Sv, j % NL, sl);
     }
     __syncthreads();
 #ifdef PP_ABL_NO_PHASE_B   // diagnostic timing build: phase A only
@@ -740,7 +746,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         const int d = c / Cv, cc = c - d * Cv;
         const int64_t v = s * D + d;              // this draw's prep record
         const int L = cc / NS, k = cc - L * NS;
-        const int j = sc_l * 3 + L;
+        const int j = sc_l * NL + L;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         const double vt = cand_speed(P, pv.ego_speed[v], k);
         const SC sc = make_sc(P, pv, Sv, v, L, vt);
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     const int64_t s = (int64_t)blockIdx.x * kWinBlock + j;
     const int64_t v0 = s * D;                 // the nominal (draw 0) prep record
     if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
-    const int NS = P.n_speeds, Cv = 3 * NS, C = D * Cv, N = P.n_points;
+    const int NS = P.n_speeds, Cv = NL * NS, C = D * Cv, N = P.n_points;
     // decision: first minimum over (lane, k) of the cost averaged over the draws (summed in draw
     // order, then / D; D = 1: the plain cost)
     int best = 0;
@@ -1017,8 +1023,8 @@ __global__ __launch_bounds__(256) void k_synth_traffic(ppsynth::LaneTables T, ui
 
 // ------------------------------------------------------------------------------------------------
 // Map::Init on the device (src/main.cpp:89-131; pp_map_create_device). g: the MapG layout
-// (13 n: ref x/y, normal x/y, lane centres x[3]/y[3], lane lengths[3]); t: the synth lane tables
-// (15 n). Three passes because each reads its neighbours' results of the previous one.
+// (kMapArrays n: ref x/y, normal x/y, lane centres x[NL]/y[NL], lane lengths[NL]); t: the synth
+// lane tables (5 NL n). Three passes because each reads its neighbours' results of the previous one.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wrap_i(int i, int n) { return i < 0 ? i + n : (i >= n ? i - n : i); }
 
@@ -1047,10 +1053,10 @@ __global__ __launch_bounds__(256) void k_map_lanes(int n, double* g) {
     ppm::sincos_pp<true>(a_avg - a_n, s_, c_);
     ax /= c_;
     ay /= c_;
-    for (int r = 0; r < 3; r++) {
+    for (int r = 0; r < NL; r++) {
         const double off = 4.0 * (r + 0.5);
         g[(4 + r) * n + i] = g[i] + ax * off;
-        g[(7 + r) * n + i] = g[n + i] + ay * off;
+        g[(4 + NL + r) * n + i] = g[n + i] + ay * off;
     }
 }
 
@@ -1058,16 +1064,16 @@ __global__ __launch_bounds__(256) void k_map_lengths(int n, double* g, double* t
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int p = wrap_i(i - 1, n);
-    for (int r = 0; r < 3; r++) {
-        const double lx = g[(4 + r) * n + i], ly = g[(7 + r) * n + i];
-        const double dx = lx - g[(4 + r) * n + p], dy = ly - g[(7 + r) * n + p];
+    for (int r = 0; r < NL; r++) {
+        const double lx = g[(4 + r) * n + i], ly = g[(4 + NL + r) * n + i];
+        const double dx = lx - g[(4 + r) * n + p], dy = ly - g[(4 + NL + r) * n + p];
         const double len = sqrt(dx * dx + dy * dy);
-        g[(10 + r) * n + i] = len;                                   // Map::get_lane_length
-        t[0 * 3 * n + r * n + i] = lx;
-        t[1 * 3 * n + r * n + i] = ly;
-        t[2 * 3 * n + r * n + i] = len;
-        t[3 * 3 * n + r * n + i] = dx / len;
-        t[4 * 3 * n + r * n + i] = dy / len;
+        g[(4 + 2 * NL + r) * n + i] = len;                           // Map::get_lane_length
+        t[0 * NL * n + r * n + i] = lx;
+        t[1 * NL * n + r * n + i] = ly;
+        t[2 * NL * n + r * n + i] = len;
+        t[3 * NL * n + r * n + i] = dx / len;
+        t[4 * NL * n + r * n + i] = dy / len;
     }
 }
 
@@ -1088,13 +1094,13 @@ namespace {
 
 constexpr int kMaxDev = 16;
 constexpr int kMaxWaypoints = 1 << 24;
-constexpr int kPrepD = 7 + 3 + 2 + 3 + 9 + 3;   // doubles per scene in PrepV (see prep_bind)
+constexpr int kPrepD = 12 + 4 * NL;   // doubles per scene in PrepV (see prep_bind)
 constexpr int kPrepI = 7;
 
 struct DevState {
     bool init = false;
-    double* map = nullptr;        // 13 * n
-    double* lanetab = nullptr;    // synth tables: lc_x[3n] lc_y[3n] seg_len[3n] tan_x[3n] tan_y[3n]
+    double* map = nullptr;        // kMapArrays * n
+    double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     void* ws = nullptr;           // prep workspace (per evaluation: scene x draw)
     int64_t ws_cap = 0;
     void* rec = nullptr;          // reference-mode winner record (per scene)
@@ -1118,9 +1124,9 @@ struct DevState {
 
 struct pp_map {
     int n = 0;
-    std::vector<double> geom;     // 13 * n (MapG layout)
-    std::vector<double> ptab;     // 10 * n: ref xy, normal, 3 lane centers (pp_map_geometry)
-    std::vector<double> lanetab;  // 15 * n
+    std::vector<double> geom;     // kMapArrays * n (MapG layout)
+    std::vector<double> ptab;     // (4 + 2 NL) * n: ref xy, normal, lane centres (pp_map_geometry)
+    std::vector<double> lanetab;  // 5 NL * n
     DevState dev[kMaxDev];
     std::mutex mu;
 };
@@ -1133,10 +1139,22 @@ struct DeviceGuard {
     ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+// pp_map_geometry's table from the MapG layout: per waypoint ref xy, normal, lane centres
+void fill_ptab(pp_map* M) {
+    const int n = M->n;
+    const double* g = M->geom.data();
+    M->ptab.assign((4 + 2 * NL) * (size_t)n, 0.0);
+    for (int i = 0; i < n; i++) {
+        double* o = &M->ptab[(4 + 2 * NL) * (size_t)i];
+        o[0] = g[i]; o[1] = g[n + i]; o[2] = g[2 * n + i]; o[3] = g[3 * n + i];
+        for (int r = 0; r < NL; r++) { o[4 + 2 * r] = g[(4 + r) * n + i]; o[5 + 2 * r] = g[(4 + NL + r) * n + i]; }
+    }
+}
+
 // Map::Init (src/main.cpp:89-131) + derived tables, on the host (done once per map).
 int build_map(pp_map* M, const double* wx, const double* wy, int n) {
     M->n = n;
-    std::vector<double> nx(n), ny(n), lcx(3 * n), lcy(3 * n);
+    std::vector<double> nx(n), ny(n), lcx(NL * n), lcy(NL * n);
     auto W = [n](int i) { return (int)(((int64_t)i + n) % n); };
     for (int i = 0; i < n; i++) {
         const int p = W(i - 1);
@@ -1154,41 +1172,36 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
         const double cos_alpha = std::cos(a_avg - a_n);
         ax /= cos_alpha;
         ay /= cos_alpha;
-        for (int r = 0; r < 3; r++) {
+        for (int r = 0; r < NL; r++) {
             const double off = 4.0 * (r + 0.5);
             lcx[r * n + i] = wx[i] + ax * off;
             lcy[r * n + i] = wy[i] + ay * off;
         }
     }
-    M->geom.assign(13 * (size_t)n, 0.0);
+    M->geom.assign(kMapArrays * (size_t)n, 0.0);
     double* g = M->geom.data();
     for (int i = 0; i < n; i++) {
         g[i] = wx[i]; g[n + i] = wy[i]; g[2 * n + i] = nx[i]; g[3 * n + i] = ny[i];
-        for (int r = 0; r < 3; r++) {
+        for (int r = 0; r < NL; r++) {
             g[(4 + r) * n + i] = lcx[r * n + i];
-            g[(7 + r) * n + i] = lcy[r * n + i];
+            g[(4 + NL + r) * n + i] = lcy[r * n + i];
             const int p = W(i - 1);
             const double dx = lcx[r * n + i] - lcx[r * n + p], dy = lcy[r * n + i] - lcy[r * n + p];
-            g[(10 + r) * n + i] = std::sqrt(dx * dx + dy * dy);    // Map::get_lane_length
+            g[(4 + 2 * NL + r) * n + i] = std::sqrt(dx * dx + dy * dy);    // Map::get_lane_length
         }
     }
-    M->ptab.assign(10 * (size_t)n, 0.0);
-    for (int i = 0; i < n; i++) {
-        double* o = &M->ptab[10 * (size_t)i];
-        o[0] = wx[i]; o[1] = wy[i]; o[2] = nx[i]; o[3] = ny[i];
-        for (int r = 0; r < 3; r++) { o[4 + 2 * r] = lcx[r * n + i]; o[5 + 2 * r] = lcy[r * n + i]; }
-    }
-    M->lanetab.assign(15 * (size_t)n, 0.0);
+    fill_ptab(M);
+    M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     double* t = M->lanetab.data();
-    for (int r = 0; r < 3; r++)
+    for (int r = 0; r < NL; r++)
         for (int i = 0; i < n; i++) {
-            const double len = g[(10 + r) * n + i];
+            const double len = g[(4 + 2 * NL + r) * n + i];
             const int p = W(i - 1);
-            t[0 * 3 * n + r * n + i] = lcx[r * n + i];
-            t[1 * 3 * n + r * n + i] = lcy[r * n + i];
-            t[2 * 3 * n + r * n + i] = len;
-            t[3 * 3 * n + r * n + i] = (lcx[r * n + i] - lcx[r * n + p]) / len;
-            t[4 * 3 * n + r * n + i] = (lcy[r * n + i] - lcy[r * n + p]) / len;
+            t[0 * NL * n + r * n + i] = lcx[r * n + i];
+            t[1 * NL * n + r * n + i] = lcy[r * n + i];
+            t[2 * NL * n + r * n + i] = len;
+            t[3 * NL * n + r * n + i] = (lcx[r * n + i] - lcx[r * n + p]) / len;
+            t[4 * NL * n + r * n + i] = (lcy[r * n + i] - lcy[r * n + p]) / len;
         }
     return PP_OK;
 }
@@ -1219,7 +1232,8 @@ ppsynth::TrafficV traffic_view(const pp_traffic* t, int64_t S) {
 
 ppsynth::LaneTables lane_tables(const double* t, int n) {
     ppsynth::LaneTables T;
-    T.n = n; T.lc_x = t; T.lc_y = t + 3 * n; T.seg_len = t + 6 * n; T.tan_x = t + 9 * n; T.tan_y = t + 12 * n;
+    T.n = n; T.lc_x = t; T.lc_y = t + NL * n; T.seg_len = t + 2 * NL * n; T.tan_x = t + 3 * NL * n;
+    T.tan_y = t + 4 * NL * n;
     return T;
 }
 
@@ -1248,10 +1262,10 @@ PrepV prep_bind(void* base, int64_t S) {
                      &p.ego_speed, &p.ego_d, &p.ego_vd, &p.in_ts, &p.in_tt};
     int k = 0;
     for (double** q : dd) *q = d + (int64_t)(k++) * S;
-    p.ratio = d + (int64_t)(k) * S; k += 3;
-    p.l_ts = d + (int64_t)(k) * S; k += 3;
-    p.l_tt = d + (int64_t)(k) * S; k += 3;
-    p.score = d + (int64_t)(k) * S; k += 3;
+    p.ratio = d + (int64_t)(k) * S; k += NL;
+    p.l_ts = d + (int64_t)(k) * S; k += NL;
+    p.l_tt = d + (int64_t)(k) * S; k += NL;
+    p.score = d + (int64_t)(k) * S; k += NL;
     // k == kPrepD
     int32_t* ip = (int32_t*)(d + (int64_t)kPrepD * S);
     int32_t** ii[] = {&p.K, &p.ref_wp, &p.T, &p.ego_lane, &p.open_mask, &p.lim_mask, &p.status};
@@ -1282,14 +1296,14 @@ int n_draws(const pp_params* p) { return p->n_draws > 1 ? p->n_draws : 1; }
 
 int cands_per_block(int C) {
     int spb = 256 / C;
-    if (spb > 21) spb = 21;      // <= 63 LDS slots per workgroup
+    if (spb > 64 / NL) spb = 64 / NL;      // <= 64 LDS spline slots per workgroup
     if (spb < 1) spb = 1;
     return spb;
 }
 
 bool params_ok(const pp_params* p) {
     return p && p->n_points > PP_PREV_KEEP && p->n_points <= PP_MAX_POINTS && p->n_speeds >= 1 &&
-           p->n_speeds <= PP_MAX_SPEEDS && 3 * p->n_speeds <= 256 &&
+           p->n_speeds <= PP_MAX_SPEEDS && NL * p->n_speeds <= 256 &&
            (p->cost_mode == PP_COST_REFERENCE || p->cost_mode == PP_COST_COMFORT) &&
            p->n_draws >= 0 && p->n_draws <= PP_MAX_DRAWS && p->noise_first_scene >= 0 &&
            !(p->n_draws > 1 && p->emit_paths);
@@ -1323,7 +1337,9 @@ void pp_params_default(pp_params* p) {
     p->noise_vel_sigma = 0.5;
 }
 
-int32_t pp_num_candidates(const pp_params* p) { return p ? n_draws(p) * 3 * p->n_speeds : 0; }
+int32_t pp_num_candidates(const pp_params* p) { return p ? n_draws(p) * NL * p->n_speeds : 0; }
+
+int32_t pp_num_lanes(void) { return NL; }
 
 double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q) {
     return ppsynth::mc_gauss(seed, (uint64_t)scene, draw, car, q);
@@ -1353,8 +1369,8 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
     DevState& D = M->dev[device];
     hipStream_t st = (hipStream_t)hip_stream;
     int* bad = nullptr;
-    if (hipMalloc(&D.map, sizeof(double) * 13 * (size_t)n) != hipSuccess ||
-        hipMalloc(&D.lanetab, sizeof(double) * 15 * (size_t)n) != hipSuccess || hipMalloc(&bad, sizeof(int)) != hipSuccess) {
+    if (hipMalloc(&D.map, sizeof(double) * kMapArrays * (size_t)n) != hipSuccess ||
+        hipMalloc(&D.lanetab, sizeof(double) * 5 * NL * (size_t)n) != hipSuccess || hipMalloc(&bad, sizeof(int)) != hipSuccess) {
         if (D.map) (void)hipFree(D.map);
         if (D.lanetab) (void)hipFree(D.lanetab);
         delete M;
@@ -1368,11 +1384,11 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
     hipLaunchKernelGGL(k_map_lengths, dim3(blocks), dim3(256), 0, st, n, D.map, D.lanetab);
     if (hipGetLastError() != hipSuccess) rc = PP_ERR_HIP;
     int hbad = 0;
-    M->geom.assign(13 * (size_t)n, 0.0);
-    M->lanetab.assign(15 * (size_t)n, 0.0);
+    M->geom.assign(kMapArrays * (size_t)n, 0.0);
+    M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     if (rc == PP_OK && (hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipMemcpyAsync(M->geom.data(), D.map, sizeof(double) * 13 * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipMemcpyAsync(M->lanetab.data(), D.lanetab, sizeof(double) * 15 * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(M->geom.data(), D.map, sizeof(double) * kMapArrays * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipMemcpyAsync(M->lanetab.data(), D.lanetab, sizeof(double) * 5 * NL * (size_t)n, hipMemcpyDeviceToHost, st) != hipSuccess ||
                         hipStreamSynchronize(st) != hipSuccess))
         rc = PP_ERR_HIP;
     (void)hipFree(bad);
@@ -1383,13 +1399,7 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
         delete M;
         return rc;
     }
-    const double* gg = M->geom.data();
-    M->ptab.assign(10 * (size_t)n, 0.0);
-    for (int i = 0; i < n; i++) {
-        double* o = &M->ptab[10 * (size_t)i];
-        o[0] = gg[i]; o[1] = gg[n + i]; o[2] = gg[2 * n + i]; o[3] = gg[3 * n + i];
-        for (int r = 0; r < 3; r++) { o[4 + 2 * r] = gg[(4 + r) * n + i]; o[5 + 2 * r] = gg[(7 + r) * n + i]; }
-    }
+    fill_ptab(M);
     D.init = true;
     *out = M;
     return PP_OK;
@@ -1414,9 +1424,9 @@ int32_t pp_map_destroy(pp_map* M) {
     return PP_OK;
 }
 
-int32_t pp_map_geometry(const pp_map* M, double* out10, int32_t n) {
-    if (!M || !out10 || n != M->n) return PP_ERR_ARG;
-    memcpy(out10, M->ptab.data(), sizeof(double) * 10 * (size_t)n);
+int32_t pp_map_geometry(const pp_map* M, double* out, int32_t n) {
+    if (!M || !out || n != M->n) return PP_ERR_ARG;
+    memcpy(out, M->ptab.data(), sizeof(double) * (4 + 2 * NL) * (size_t)n);
     return PP_OK;
 }
 
@@ -1504,7 +1514,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const int64_t blocks = (Sv + threads - 1) / threads;
         if (timing) (void)hipEventRecord(ev[0], st);
         if (mg.n <= kLdsMapMax) {
-            const size_t lds = sizeof(double) * 13 * (size_t)mg.n;
+            const size_t lds = sizeof(double) * kMapArrays * (size_t)mg.n;
             hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status);
         } else {
             hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status);
@@ -1514,11 +1524,11 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     {
         // a block holds SPB whole scenes (all draws: the spline slots are shared by the draws),
         // or, when a scene has more than 256 candidates, BPS blocks share one scene
-        const int C = Dn * 3 * P.n_speeds;
+        const int C = Dn * NL * P.n_speeds;
         const int spb = C <= 256 ? cands_per_block(C) : 1;
         const int bps = C <= 256 ? 1 : (C + 255) / 256;
         const int threads = C <= 256 ? ((spb * C + 63) / 64) * 64 : 256;
-        const int nslot = 3 * spb;
+        const int nslot = NL * spb;
         const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
         const int64_t blocks = bps == 1 ? (S + spb - 1) / spb : S * bps;
         if (blocks > 0x7fffffff) return PP_ERR_ARG;
@@ -1699,7 +1709,7 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     const int64_t S = hin->n_scenes;
     if (S == 0) return PP_OK;
     const int J = hin->car_stride, N = prm->n_points;
-    const int C = n_draws(prm) * 3 * prm->n_speeds;
+    const int C = n_draws(prm) * NL * prm->n_speeds;
     const bool tab = hin->tab_valid != nullptr;
     // staging layout: doubles first, then 4-byte fields
     const size_t nd = (size_t)S * (4 + 2 * PP_PREV_KEEP + 4 * J + (tab ? 6 * PP_MAX_CARS : 0) + 2 * N + C);
@@ -1806,7 +1816,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         device < 0 || device >= kMaxDev || (n_prev > 0 && (!prev_x || !prev_y)) ||
         (n_cars > 0 && (!car_id || !car_x || !car_y || !car_vx || !car_vy)))
         return PP_ERR_ARG;
-    if (*target_lane < 0 || *target_lane > 2) return PP_ERR_ARG;
+    if (*target_lane < 0 || *target_lane >= NL) return PP_ERR_ARG;
     // host staging: one scene, SoA with S = 1 (std::map order: stable sort by id, last row of a
     // duplicated id wins as in `sensor_fusion_cars[id]` assignment, src/main.cpp:1329)
     struct Row { int32_t id; double x, y, vx, vy; };
@@ -1823,7 +1833,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     struct Frame {
         double ego[4], px[PP_PREV_KEEP], py[PP_PREV_KEEP], cx[PP_MAX_CARS], cy[PP_MAX_CARS],
             cvx[PP_MAX_CARS], cvy[PP_MAX_CARS];
-        double nx[N], ny[N], cost[3];
+        double nx[N], ny[N], cost[NL];
         DevState::PlanTab tab;
         int32_t nprev, ptl, ncars, cid[PP_MAX_CARS], winner, nout;
         uint32_t status;

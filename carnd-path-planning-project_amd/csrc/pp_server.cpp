@@ -206,7 +206,7 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
     int64_t frames = 0, ticks = 0, accepted = 0, replies = 0;
     int32_t rc = PP_OK;
     const int cap = o->max_clients;
-    const int J = PP_MAX_CARS, N = prm.n_points, C = 3 * prm.n_speeds;
+    const int J = PP_MAX_CARS, N = prm.n_points, C = PP_NUM_LANES * prm.n_speeds;
     // host batch (SoA, cap scenes) + results
     std::vector<double> ego(4 * cap), pxy(2 * PP_PREV_KEEP * cap), cars(4 * J * cap), tabd(6 * PP_MAX_CARS * cap);
     std::vector<int32_t> ints(3 * cap), cid(J * cap), tabi(2 * PP_MAX_CARS * cap), mst(cap);

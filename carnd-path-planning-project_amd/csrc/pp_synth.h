@@ -6,18 +6,23 @@
 // so host and device outputs are bit-identical except ego_yaw_deg.
 //
 // Scene model (a highway snapshot around the ego):
-//   ego on lane r at a uniform point of the 181-waypoint loop, |d jitter| <= 0.3 m, speed U[0, 22.2]
+//   ego on lane r (of PP_NUM_LANES) at a uniform point of the 181-waypoint loop, |d jitter| <= 0.3 m, speed U[0, 22.2]
 //   (5 %: U[0, 3]), longitudinal accel U(-3, 3), 30 % of scenes drift laterally (U(-2, 2) m/s);
 //   previous path = 10 points behind the ego along its lane, spacing v/50 (p9 = ego);
 //   1 % of scenes are "frame 0" (n_prev = 0, telemetry pose only);
 //   prev_target_lane = ego lane, 20 % an adjacent lane;
 //   12 cars, ids 0..11, ds ~ U(-60, 250) m along their lane (2 %: half a loop away, usually
-//   unmatchable), lane U{0,1,2}, d jitter +-0.3, speed U(5, 25) along the lane tangent, vd ~ N(0, 0.3).
+//   unmatchable), lane U{0..PP_NUM_LANES-1}, d jitter +-0.3, speed U(5, 25) along the lane tangent, vd ~ N(0, 0.3).
 #pragma once
 #include <stdint.h>
 #include <math.h>
 
+#ifndef PP_HD
 #define PP_HD __host__ __device__
+#endif
+#ifndef PP_NUM_LANES
+#define PP_NUM_LANES 3
+#endif
 
 namespace ppsynth {
 
@@ -186,7 +191,7 @@ PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int
     const int n = T.n;
     const int seg = r.below(n);
     const double t = r.uni();
-    const int lane = r.below(3);
+    const int lane = r.below(PP_NUM_LANES);
     const double djit = r.uni(-0.3, 0.3);
     double v = r.uni(0.0, 22.2);
     if (r.uni() < 0.05) v = r.uni(0.0, 3.0);
@@ -197,7 +202,7 @@ PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int
     if (r.uni() < 0.2) {
         const int dir = (r.uni() < 0.5) ? -1 : 1;
         ptl = lane + dir;
-        if (ptl < 0 || ptl > 2) ptl = lane - dir;
+        if (ptl < 0 || ptl > PP_NUM_LANES - 1) ptl = lane - dir;
     }
     // previous path: p9 = ego; p_{9-k} walked back sum_{m<k} spacing_m along the lane
     double back = 0.0;
@@ -226,7 +231,7 @@ PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int
         const int64_t ix = (int64_t)j * S + local;
         double ds = r.uni(-60.0, 250.0);
         if (r.uni() < 0.02) ds = 0.5 * 6945.554;
-        const int cl = r.below(3);
+        const int cl = r.below(PP_NUM_LANES);
         const double cd = r.uni(-0.3, 0.3);
         const double cs = r.uni(5.0, 25.0);
         const double cvd = 0.3 * r.gauss();

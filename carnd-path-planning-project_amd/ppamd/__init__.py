@@ -18,7 +18,23 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PPAMD_LIB") or os.path.join(_HERE, "libppamd.so")   # override: A/B builds
 
-NUM_LANES = 3
+def _open():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"ppamd: HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+    # torch (ROCm) bundles its own libamdhip64 (soname libamdhip64.so.7, loaded by path). Load it
+    # first so that our DT_NEEDED libamdhip64.so.7 resolves to that same runtime: two HIP runtimes
+    # in one process do not share device allocations.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    h = C.CDLL(LIB_PATH)
+    h.pp_num_lanes.restype = C.c_int32
+    return h
+
+
+_LIB = _open()
+NUM_LANES = int(_LIB.pp_num_lanes())   # PP_NUM_LANES the library was built for (src/main.cpp:22)
 PREV_KEEP = 10
 MAX_CARS = 16
 MAX_SPEEDS = 8
@@ -90,15 +106,15 @@ class Params(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [("ego_x", C.c_double), ("ego_y", C.c_double), ("ego_speed", C.c_double),
                 ("ego_acc", C.c_double), ("ego_s", C.c_double), ("ego_d", C.c_double),
-                ("ego_vs", C.c_double), ("ego_vd", C.c_double), ("ref_ratio", C.c_double * 3),
-                ("lane_score", C.c_double * 3), ("ref_wp", C.c_int32), ("ego_lane", C.c_int32),
+                ("ego_vs", C.c_double), ("ego_vd", C.c_double), ("ref_ratio", C.c_double * NUM_LANES),
+                ("lane_score", C.c_double * NUM_LANES), ("ref_wp", C.c_int32), ("ego_lane", C.c_int32),
                 ("target_lane", C.c_int32), ("lane_open_mask", C.c_int32),
                 ("n_matched_cars", C.c_int32), ("in_lane_car", C.c_int32), ("_pad", C.c_int32 * 2)]
 
 
 INFO_DTYPE = np.dtype([("ego_x", "f8"), ("ego_y", "f8"), ("ego_speed", "f8"), ("ego_acc", "f8"),
                        ("ego_s", "f8"), ("ego_d", "f8"), ("ego_vs", "f8"), ("ego_vd", "f8"),
-                       ("ref_ratio", "f8", 3), ("lane_score", "f8", 3), ("ref_wp", "i4"),
+                       ("ref_ratio", "f8", NUM_LANES), ("lane_score", "f8", NUM_LANES), ("ref_wp", "i4"),
                        ("ego_lane", "i4"), ("target_lane", "i4"), ("lane_open_mask", "i4"),
                        ("n_matched_cars", "i4"), ("in_lane_car", "i4"), ("_pad", "i4", 2)])
 assert INFO_DTYPE.itemsize == C.sizeof(SceneInfo)
@@ -117,20 +133,12 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_synth_scenes", "pp_synth_scenes_host", "pp_timing_enable", "pp_timing_read",
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
-           "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device"]
+           "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device",
+           "pp_num_lanes"]
 
 
 def _load():
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"ppamd: HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
-    # torch (ROCm) bundles its own libamdhip64 (soname libamdhip64.so.7, loaded by path). Load it
-    # first so that our DT_NEEDED libamdhip64.so.7 resolves to that same runtime: two HIP runtimes
-    # in one process do not share device allocations.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
-    lib = C.CDLL(LIB_PATH)
+    lib = _LIB
     lib.pp_params_default.argtypes = [C.POINTER(Params)]
     lib.pp_params_default.restype = None
     lib.pp_num_candidates.argtypes = [C.POINTER(Params)]
@@ -267,7 +275,7 @@ class Map:
         return self
 
     def geometry(self) -> np.ndarray:
-        out = np.zeros((self.n, 10), np.float64)
+        out = np.zeros((self.n, 4 + 2 * NUM_LANES), np.float64)
         _check(lib.pp_map_geometry(self.handle, out.ctypes.data_as(_dp), self.n), "pp_map_geometry")
         return out
 
@@ -441,7 +449,7 @@ def synth_device(m: Map, S, seed=0x5EED0001, first=0, device=0, stream=None, car
 
 def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
     D = max(prm.n_draws, 1)
-    Cn = D * 3 * prm.n_speeds
+    Cn = D * NUM_LANES * prm.n_speeds
     N = prm.n_points
     if xp == "numpy":
         mk = lambda sh, dt: np.zeros(sh, dt)
@@ -457,7 +465,7 @@ def alloc_result(S, prm: Params, xp="numpy", device=None, info=False):
         r["paths"] = mk((S, N, Cn, 2), f8)
         r["path_len"] = mk((S, Cn), i4)
     if D > 1:
-        r["draw_mean_cost"] = mk((S, 3 * prm.n_speeds), f8)
+        r["draw_mean_cost"] = mk((S, NUM_LANES * prm.n_speeds), f8)
     if info:
         if xp == "numpy":
             r["info"] = np.zeros((S,), INFO_DTYPE)

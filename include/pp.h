@@ -30,7 +30,9 @@ extern "C" {
 #endif
 
 /* ---- fixed sizes ------------------------------------------------------------------------- */
-#define PP_NUM_LANES   3    /* src/main.cpp:22 NUM_LANES                                      */
+#ifndef PP_NUM_LANES        /* src/main.cpp:22 NUM_LANES (a build-time constant there too; the */
+#define PP_NUM_LANES   3    /* library is built for one value: pp_num_lanes() reports it)      */
+#endif
 #define PP_PREV_KEEP   10   /* src/main.cpp:1258 prev_trajectory_length                       */
 #define PP_MAX_CARS    16   /* sensor_fusion rows per scene (simulator sends 12)              */
 #define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
@@ -178,6 +180,7 @@ typedef struct pp_map pp_map;
 
 void    pp_params_default(pp_params* p);
 int32_t pp_num_candidates(const pp_params* p);
+int32_t pp_num_lanes(void);           /* PP_NUM_LANES of this build */
 
 /* Map::Init (src/main.cpp:89-131) on the host (bit-identical to the reference's); the lane
  * geometry is uploaded lazily per device. n >= 3 waypoints, any size. */
@@ -190,8 +193,8 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
                              pp_map** out);
 int32_t pp_map_destroy(pp_map* m);
 /* host copy of the derived geometry: per waypoint {ref.x, ref.y, nx, ny, lc0.x, lc0.y, lc1.x,
- * lc1.y, lc2.x, lc2.y} (10 doubles) — the Map::Init known-answer output. */
-int32_t pp_map_geometry(const pp_map* m, double* out10, int32_t n);
+ * lc1.y, ...} (4 + 2 * PP_NUM_LANES doubles) — the Map::Init known-answer output. */
+int32_t pp_map_geometry(const pp_map* m, double* out, int32_t n);
 
 /* Pre-size the per-device workspace (optional; pp_eval grows it on demand, which allocates). */
 int32_t pp_reserve(pp_map* m, int32_t device, int64_t max_scenes);

@@ -165,7 +165,7 @@ static int lane_matching(const OMap* m, const OFrame* f, double x, double y, dou
     P2 p = {x, y};
     int stop = 0;
     int cur = f->ref_wp;
-    double sum_s[PP_NUM_LANES] = {0, 0, 0};
+    double sum_s[PP_NUM_LANES] = {0};
     double s_ratio[PP_NUM_LANES];
     for (int i = 0; i < PP_NUM_LANES; i++) s_ratio[i] = f->ratio[i];
     double best = 1000 * 1000;
@@ -336,7 +336,8 @@ static int calc_target_lane(const pp_params* P, const OCar* cars, int nc, int eg
         score_out[lane] = total;
         if (total > best_score) { best_score = total; best_lane = lane; }
     }
-    *open_mask = open[0] | (open[1] << 1) | (open[2] << 2);
+    *open_mask = 0;
+    for (int lane = 0; lane < PP_NUM_LANES; lane++) *open_mask |= open[lane] << lane;
     *jump_rule = 0;
     if (abs(ego_lane - best_lane) > 1) {
         int nl = best_lane > ego_lane ? ego_lane + 1 : ego_lane - 1;
@@ -644,7 +645,7 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
     int T = calc_target_lane(P, cars, nc, ego_lane, in->prev_target_lane[s], ego_s, ego_vs,
                              pr->dt0, pr->score, &pr->open_mask, &jump);   /* :1352-1356 */
     if (jump) pr->status |= PP_ST_JUMP_RULE;
-    if (pr->open_mask != 7) pr->status |= PP_ST_LANE_CLOSED;
+    if (pr->open_mask != (1 << PP_NUM_LANES) - 1) pr->status |= PP_ST_LANE_CLOSED;
     if (T != ego_lane) {                                                /* :1358-1369 */
         double dtl = lane_offset(T);
         double diff = fabs(ego_vd * 1.0 + ego_d - dtl);
@@ -653,8 +654,9 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
     /* follow-car selection (:1383-1411), for the in-lane car and for every candidate lane */
     int in_k = -1;
     double in_s = 0;
-    int tk[PP_NUM_LANES] = {-1, -1, -1};
-    double ts_[PP_NUM_LANES] = {0, 0, 0};
+    int tk[PP_NUM_LANES];
+    double ts_[PP_NUM_LANES];
+    for (int L = 0; L < PP_NUM_LANES; L++) { tk[L] = -1; ts_[L] = 0; }
     for (int k = 0; k < nc; k++) {
         double s0 = cars[k].s + cars[k].vs * pr->dt0;
         double d0 = cars[k].d + cars[k].vd * pr->dt0;
@@ -923,13 +925,13 @@ static OSC make_sc(const pp_params* P, const OPrep* pr, int L, double v) {
 /* ------------------------------------------------------------------------------------------ */
 /* exported oracle API (ctypes)                                                                */
 /* ------------------------------------------------------------------------------------------ */
-int ppo_map_geometry(const double* wx, const double* wy, int n, double* out10) {
+int ppo_map_geometry(const double* wx, const double* wy, int n, double* out) {
     OMap m;
     if (n < 2 || omap_init(&m, wx, wy, n)) return -1;
     for (int i = 0; i < n; i++) {
-        double* o = out10 + 10 * i;
+        double* o = out + (4 + 2 * PP_NUM_LANES) * i;
         o[0] = m.ref[i].x; o[1] = m.ref[i].y; o[2] = m.nx[i]; o[3] = m.ny[i];
-        for (int r = 0; r < 3; r++) { o[4 + 2 * r] = m.lc[i][r].x; o[5 + 2 * r] = m.lc[i][r].y; }
+        for (int r = 0; r < PP_NUM_LANES; r++) { o[4 + 2 * r] = m.lc[i][r].x; o[5 + 2 * r] = m.lc[i][r].y; }
     }
     omap_free(&m);
     return 0;
@@ -1018,7 +1020,7 @@ int ppo_eval_range(const double* wx, const double* wy, int n_wp, const pp_scene_
             memset(I, 0, sizeof(*I));
             I->ego_x = pr.ego_x; I->ego_y = pr.ego_y; I->ego_speed = pr.ego_speed; I->ego_acc = pr.ego_acc;
             I->ego_s = pr.ego_s; I->ego_d = pr.ego_d; I->ego_vs = pr.ego_vs; I->ego_vd = pr.ego_vd;
-            for (int l = 0; l < 3; l++) { I->ref_ratio[l] = pr.fr.ratio[l]; I->lane_score[l] = pr.score[l]; }
+            for (int l = 0; l < PP_NUM_LANES; l++) { I->ref_ratio[l] = pr.fr.ratio[l]; I->lane_score[l] = pr.score[l]; }
             I->ref_wp = pr.fr.ref_wp; I->ego_lane = pr.ego_lane; I->target_lane = pr.T;
             I->lane_open_mask = pr.open_mask; I->n_matched_cars = pr.nmatched; I->in_lane_car = pr.in_id;
         }
@@ -1032,6 +1034,8 @@ int ppo_eval(const double* wx, const double* wy, int n_wp, const pp_scene_batch*
              const pp_params* P, pp_result* out) {
     return ppo_eval_range(wx, wy, n_wp, in, P, out, 0, in ? in->n_scenes : 0);
 }
+
+int ppo_num_lanes(void) { return PP_NUM_LANES; }
 
 int ppo_struct_sizes(int64_t* out4) {
     out4[0] = sizeof(pp_scene_batch);
@@ -1049,10 +1053,10 @@ typedef struct { double *len, *tx, *ty; int n; const OMap* m; } OLanes;   /* [la
 static void olanes_init(OLanes* L, const OMap* m) {
     const int n = m->n;
     L->n = n; L->m = m;
-    L->len = (double*)malloc(sizeof(double) * 3 * n);
-    L->tx = (double*)malloc(sizeof(double) * 3 * n);
-    L->ty = (double*)malloc(sizeof(double) * 3 * n);
-    for (int r = 0; r < 3; r++)
+    L->len = (double*)malloc(sizeof(double) * PP_NUM_LANES * n);
+    L->tx = (double*)malloc(sizeof(double) * PP_NUM_LANES * n);
+    L->ty = (double*)malloc(sizeof(double) * PP_NUM_LANES * n);
+    for (int r = 0; r < PP_NUM_LANES; r++)
         for (int i = 0; i < n; i++) {
             const int q = wpi(m, i - 1);
             const double dx = m->lc[i][r].x - m->lc[q][r].x, dy = m->lc[i][r].y - m->lc[q][r].y;

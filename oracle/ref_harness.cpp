@@ -58,7 +58,7 @@ extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_s
     vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
     map.Init(X, Y);
     const int64_t S = in->n_scenes;
-    const int C = 3 * n_speeds;
+    const int C = NUM_LANES * n_speeds;
     for (int64_t s = 0; s < S; s++) {
         double ego_x = in->ego_x[s];
         double ego_y = in->ego_y[s];
@@ -260,6 +260,8 @@ static void rollout_frame(Map& map, std::map<int, Car>& sensor_fusion_cars, cons
 
 }  // namespace refh
 
+extern "C" int ref_num_lanes() { return NUM_LANES; }
+
 // in: host telemetry batch (updated in place; its tab_* are not used: the std::map is the table)
 extern "C" int ref_rollout(const double* wx, const double* wy, int n_wp, pp_scene_batch* in,
                            pp_traffic* tr, const pp_rollout_cfg* cfg, pp_rollout_log* log) {
@@ -267,8 +269,8 @@ extern "C" int ref_rollout(const double* wx, const double* wy, int n_wp, pp_scen
     vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
     map.Init(X, Y);
     const int n = (int)map.waypoints.size();
-    vector<double> len(3 * n), tx(3 * n), ty(3 * n);
-    for (int r = 0; r < 3; r++)
+    vector<double> len(NUM_LANES * n), tx(NUM_LANES * n), ty(NUM_LANES * n);
+    for (int r = 0; r < NUM_LANES; r++)
         for (int i = 0; i < n; i++) {
             const int q = (i - 1 + n) % n;
             const Point a = map.waypoints[q].lane_center[r], b = map.waypoints[i].lane_center[r];

@@ -21,8 +21,9 @@ if PKG not in sys.path:
 
 import ppamd  # noqa: E402  (structures shared with the C-ABI)
 
-ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
-REF_SO = os.path.join(REPO, "oracle", "_ref", "libppref.so")
+# overrides select the builds for another PP_NUM_LANES (tests/test_lanes.py)
+ORACLE_SO = os.environ.get("PP_ORACLE_SO") or os.path.join(REPO, "oracle", "liboracle.so")
+REF_SO = os.environ.get("PP_REF_SO") or os.path.join(REPO, "oracle", "_ref", "libppref.so")
 REF_JSON_SO = os.path.join(REPO, "oracle", "_ref", "libppref_json.so")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
@@ -44,6 +45,8 @@ def load_oracle():
                                 C.POINTER(ppamd.Params), C.POINTER(ppamd.RolloutCfg), C.POINTER(ppamd.Result),
                                 C.POINTER(ppamd.RolloutLog)]
     lib.ppo_rollout.restype = C.c_int
+    lib.ppo_num_lanes.restype = C.c_int
+    assert lib.ppo_num_lanes() == ppamd.NUM_LANES, (ORACLE_SO, ppamd.LIB_PATH)
     return lib
 
 
@@ -88,6 +91,8 @@ def load_ref():
     lib.ref_rollout.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.POINTER(ppamd.Traffic),
                                 C.POINTER(ppamd.RolloutCfg), C.POINTER(ppamd.RolloutLog)]
     lib.ref_rollout.restype = C.c_int
+    lib.ref_num_lanes.restype = C.c_int
+    assert lib.ref_num_lanes() == ppamd.NUM_LANES, (REF_SO, ppamd.LIB_PATH)
     return lib
 
 
@@ -152,7 +157,7 @@ def oracle_eval(lib, wx, wy, scenes, prm, begin=0, end=None, info=True):
 def ref_eval(lib, wx, wy, scenes, n_speeds, speed_offsets, with_frame=True):
     """Run the reference-compiled checker (N = 50 only: the reference hard-codes it)."""
     S = int(scenes["ego_x"].shape[0])
-    Cn = 3 * n_speeds
+    Cn = ppamd.NUM_LANES * n_speeds
     out = {"ref_next": np.zeros((S, 50, 2)), "ref_n": np.zeros(S, np.int32),
            "ref_T": np.zeros(S, np.int32), "paths": np.full((S, Cn, 50, 2), np.nan),
            "path_len": np.zeros((S, Cn), np.int32), "info": np.zeros((S, 8))}

@@ -47,7 +47,7 @@ def test_montecarlo_equals_materialised_draws(cpu, mode, n_speeds, D):
     sc = ppamd.synth_host(cpu["m"], S, seed=0xC0FFEE)
     prm = ppamd.default_params(n_speeds=n_speeds, cost_mode=mode, n_draws=D, noise_first_scene=1000)
     mc = oracle_lib.oracle_eval(olib, wx, wy, sc, prm)
-    Cv = 3 * n_speeds
+    Cv = ppamd.NUM_LANES * n_speeds
     assert mc["cost"].shape == (S, D * Cv)
     status = np.zeros(S, np.uint32)
     nominal = None
@@ -80,7 +80,7 @@ def test_montecarlo_equals_materialised_draws(cpu, mode, n_speeds, D):
         Ts = np.stack([oracle_lib.oracle_eval(olib, wx, wy, oracle_lib.noisy_scenes(olib, sc, prm, d),
                                               ppamd.default_params(n_speeds=1), info=True)["info"]["target_lane"]
                        for d in range(D)], 1)
-        counts = np.stack([(Ts == L).sum(1) for L in range(3)], 1)
+        counts = np.stack([(Ts == L).sum(1) for L in range(ppamd.NUM_LANES)], 1)
         assert (counts[np.arange(S), win // n_speeds] == counts.max(1)).all()
 
 
@@ -133,7 +133,7 @@ class TestMonteCarloGPU:
         prm = ppamd.default_params(n_speeds=n_speeds, cost_mode=mode, n_draws=D)
         got = self.run(env, sc_dev, prm)
         ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
-        self.check(got, ref, D, 3 * n_speeds)
+        self.check(got, ref, D, ppamd.NUM_LANES * n_speeds)
 
     def test_shard_offset(self, env):
         """noise_first_scene makes a shard's draws those of the same scenes in the full batch."""
