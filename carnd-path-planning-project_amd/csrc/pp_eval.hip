@@ -48,6 +48,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
     return m;
 }
 
+#ifndef PP_ANGLE_CROSS
+#define PP_ANGLE_CROSS 1
+#endif
 #ifndef PP_PREP_WAVES
 #define PP_PREP_WAVES 3
 #endif
@@ -538,7 +541,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     int cnt = 0;                     // #knots with X < x (std::lower_bound position)
     // cached segment: valid while seg_lo < x <= seg_hi (NaN x never valid)
     double seg_lo = 1.0, seg_hi = 0.0, sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
-    double arg = 0, prev_speed = sc.start, prev_angle = 0;
+    double arg = 0, prev_speed = sc.start;
+#if PP_ANGLE_CROSS
+    double uxp = 1.0, uyp = 0.0;     // previous step direction (angle 0: the local frame's x axis)
+#else
+    double prev_angle = 0;
+#endif
     while (arg < 50 && ng < room) {
         double speed = sc_get_speed(sc, cur_t);
         double dstep = speed / 50;
@@ -559,12 +567,25 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         else y = ((sa_ * h + sb) * h + sc_) * h + sy;
         const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
         double acc = fabs(speed - prev_speed) * 50;
-#ifdef PP_ABL_NO_ATAN     // diagnostic timing build
-        const double astep = (y - pos_y) * (x - pos_x);
+#if PP_ANGLE_CROSS
+        // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
+        // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
+        double ux, uy;
+        {
+            const double ddx = x - pos_x, ddy = y - pos_y;
+            const double r = ppm::rcp_nr(d);
+            ux = ddx * r; uy = ddy * r;
+            if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
+        }
+        const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
+        double adt;
+        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1)) adt = ppm::asin_small(cr);
+        else adt = ppm::atan2_fast(cr, dt);
+        const double adiff = ppm::fmod_2pi(adt + 3 * kPi) - kPi;
 #else
         const double astep = ppm::atan2_fast(y - pos_y, x - pos_x);
-#endif
         const double adiff = ppm::fmod_2pi(astep - prev_angle + 3 * kPi) - kPi;
+#endif
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
         if (acc + cacc > P.maximum_acc) {
@@ -612,7 +633,11 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         }
         cur_t += 0.02;
         prev_speed = speed;
+#if PP_ANGLE_CROSS
+        uxp = ux; uyp = uy;
+#else
         prev_angle = astep;
+#endif
         const double sp_step = (x - pos_x) * dstep / d;
         pos_y += (y - pos_y) * dstep / d;
         arg += sp_step;

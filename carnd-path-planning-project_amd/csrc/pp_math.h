@@ -239,6 +239,35 @@ __device__ __forceinline__ double atan2_fast(double y, double x) {
     return m == 0 ? zz : m == 1 ? -zz : m == 2 ? pi - (zz - pi_lo) : (zz - pi_lo) - pi;
 }
 
+// Angle between consecutive step directions without atan2 (run_candidate). The reference turns
+// each step (dx, dy) into an absolute angle atan2(dy, dx) and wraps the difference to the previous
+// one (src/main.cpp:934). For unit vectors u_prev, u the signed angle is asin(u_prev x u) while
+// u_prev . u > 0 and |u_prev x u| <= kStepSinMax (|angle| <= 0.0708 rad): the Taylor series through
+// s^13 is then accurate to ~1e-18 relative (next term c7 s^15 < 1.1e-18 s), and the unit vectors
+// carry ~2 ulp, so the angle differs from atan2(dy,dx) - atan2(dy',dx') by < 1e-17 rad. The caller
+// applies the reference's wrap fmod(. + 3 pi, 2 pi) - pi to it, whose rounding grid (ulp(3 pi) =
+// 1.8e-15) dominates, exactly as it does for the reference's own difference of two atan2 values.
+constexpr double kStepSinMax = 0.0708;
+__device__ __forceinline__ double asin_small(double s) {
+    const double c1 = 1.66666666666666666667e-01, c2 = 7.50000000000000000000e-02,
+                 c3 = 4.46428571428571428571e-02, c4 = 3.03819444444444444444e-02,
+                 c5 = 2.23721590909090909091e-02, c6 = 1.73527644230769230769e-02;
+    const double z = s * s;
+    double p = __builtin_fma(z, c6, c5);
+    p = __builtin_fma(z, p, c4);
+    p = __builtin_fma(z, p, c3);
+    p = __builtin_fma(z, p, c2);
+    p = __builtin_fma(z, p, c1);
+    return __builtin_fma(s * z, p, s);
+}
+// 1/d to ~1 ulp: v_rcp_f64 and two Newton steps (d finite, normal)
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    return r;
+}
+
 // fmod(a, 2*pi) for the reference's angle wrap fmod(d + 3*pi, 2*pi) - pi
 // (src/main.cpp:870, 934). fmod is exact, so any exact evaluation is bit-identical: for
 // 0 <= a < 3*(2*pi) the remainder a - k*(2*pi), k in {0, 1, 2}, is computed exactly
