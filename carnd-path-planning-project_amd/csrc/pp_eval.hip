@@ -40,6 +40,7 @@ struct MapG { const double* buf; int n; };
 // <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
 constexpr double kSlowAngle = 1.0e5;
 constexpr int kLimSlow = 1 << 7;   // internal bit in PrepV.lim_mask
+static_assert(NL <= 6, "lim_mask: bit 0 in-lane limit, bits 1..NL lane limits, bit 7 kLimSlow");
 
 __device__ __forceinline__ MapV map_view(const double* b, int n) {
     MapV m;
@@ -48,8 +49,19 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
     return m;
 }
 
+#ifndef PP_TEAM_SETUP
+#define PP_TEAM_SETUP 1
+#endif
+#ifndef PP_SEG_MODE
+#define PP_SEG_MODE 0
+#endif
 #ifndef PP_ANGLE_CROSS
 #define PP_ANGLE_CROSS 1
+#endif
+// Divisions of the candidate loop as a reciprocal and one correction step (ppm::div_rcp):
+// bit 0: the two divisions by the step length d, bit 1: speed / 50, bit 2: the speed ramp / ttime
+#ifndef PP_DIV_RCP
+#define PP_DIV_RCP 7
 #endif
 #ifndef PP_PREP_WAVES
 #define PP_PREP_WAVES 3
@@ -468,6 +480,170 @@ __device__ void setup_lane(const MapV& m, const pp_params& P, const pp_scene_bat
 }
 
 // ------------------------------------------------------------------------------------------------
+// Phase A by a team of TS threads per slot (k_cand): setup_lane's arithmetic, element for element,
+// with its point- and row-local parts spread over the team and only the two band sweeps serial:
+//   A1 (team)  previous-path knots; control point k: its own Map::get_lane_pos call (the reference
+//              makes one call per point, :744-768) -> global xy in a(npk+1+k)/b(npk+1+k), ok in
+//              c(npk+1+k), local xy in x/y(npk+1+k);
+//   A2 (r = 0) the distance rule over the control points (:762), knot truncation, fallback, meta;
+//   A3 (team)  each band row's preconditioned terms: a = up/dg, c = lo/dg, b = rhs/dg;
+//   A4 (r = 0) Gauss + l_solve forward, r_solve backward (one division per row each way);
+//   A5 (team)  the segment coefficients (spline.h:345-349) and the last row (:367-370).
+// The caller puts a block barrier between the steps.
+// ------------------------------------------------------------------------------------------------
+struct LaneGeom {
+    int K, npk, ref_wp;
+    double pos_x, pos_y, ca, sa, dist, min_cpd, ratio, ego_d;
+};
+__device__ __forceinline__ LaneGeom lane_geom(const PrepV& pv, int64_t v, int64_t Sv, int L) {
+    LaneGeom g;
+    g.K = pv.K[v];
+    g.npk = g.K > 0 ? g.K - 1 : 0;
+    g.pos_x = pv.pos_x[v]; g.pos_y = pv.pos_y[v];
+    g.ca = pv.ca_m[v]; g.sa = pv.sa_m[v];
+    g.ref_wp = pv.ref_wp[v];
+    g.ratio = pv.ratio[L * Sv + v];
+    g.ego_d = pv.ego_d[v];
+    const double start = pv.ego_speed[v], ego_vd = pv.ego_vd[v];
+    double min_cpd = start * 1;
+    g.min_cpd = s_max(min_cpd, 5.0);
+    const double d_diff = lane_offset(L) - g.ego_d;
+    const double d_acc = 4;
+    bool slow = false;
+    double lst = 2.0;
+    if ((ego_vd < 0) == (d_diff < 0)) {
+        const double dmax = ego_vd * ego_vd / d_acc / 2;
+        if (dmax > fabs(d_diff)) { slow = true; lst = fabs(ego_vd) / d_acc; }
+    }
+    if (!slow) {
+        double rel = ego_vd;
+        if (d_diff < 0) rel *= -1;
+        const double add = fabs(d_diff);
+        const double peak = sqrt(add * d_acc + rel * rel / 2);
+        lst = (peak * 2 - rel) / d_acc;
+    }
+    double dist = start * lst;
+    if (dist < 10.0) dist = 10.0;
+    if (dist > 50) dist = 50;
+    g.dist = dist;
+    return g;
+}
+
+__device__ void team_a1(const MapV& m, const pp_scene_batch& in, const LaneGeom& g, int64_t s, int L,
+                        const Slot& sl, int r, int TS) {
+    const int64_t S = in.n_scenes;
+    for (int i = r; i < g.npk; i += TS) {
+        const double tx0 = in.prev_x[(int64_t)i * S + s] - g.pos_x;
+        const double ty0 = in.prev_y[(int64_t)i * S + s] - g.pos_y;
+        sl.x(i) = tx0 * g.ca - ty0 * g.sa;
+        sl.y(i) = tx0 * g.sa + ty0 * g.ca;
+    }
+    if (r == 0) {
+        sl.x(g.npk) = (g.pos_x - g.pos_x) * g.ca - (g.pos_y - g.pos_y) * g.sa;
+        sl.y(g.npk) = (g.pos_x - g.pos_x) * g.sa + (g.pos_y - g.pos_y) * g.ca;
+    }
+    for (int k = r; k < 5; k += TS) {
+        double cps = g.dist;
+        for (int i = 1; i <= k; i++) cps = cps + g.min_cpd;
+        double px, py;
+        bool ok;
+        get_lane_pos(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
+        const int j = g.npk + 1 + k;
+        sl.a(j) = px; sl.b(j) = py; sl.c(j) = ok ? 1.0 : 0.0;
+        const double tx0 = px - g.pos_x, ty0 = py - g.pos_y;
+        sl.x(j) = tx0 * g.ca - ty0 * g.sa;
+        sl.y(j) = tx0 * g.sa + ty0 * g.ca;
+    }
+}
+
+__device__ void team_a2(const LaneGeom& g, const Slot& sl) {
+    int flags = 0;
+    double lx = g.pos_x, ly = g.pos_y, total = 0;
+    int ncp = 1;
+    for (int i = 0; i < 5; i++) {
+        const int j = g.npk + 1 + i;
+        const double npx = sl.a(j), npy = sl.b(j);
+        if (sl.c(j) == 0.0) flags |= kMetaWalkFail;
+        total += sqrt((npx - lx) * (npx - lx) + (npy - ly) * (npy - ly));
+        lx = npx; ly = npy;
+        ncp++;
+        if (total > 50 && ncp > 2) break;
+    }
+    int nk = g.npk + ncp;
+    for (int i = 1; i < nk; i++) {                                      // :833-843
+        if (sl.x(i) <= sl.x(i - 1)) { nk = i; flags |= kMetaTrunc; break; }
+    }
+    const bool fallback = nk < 3 || nk <= g.npk || fabs(g.ego_d) > 20;  // :848
+    if (fallback) flags |= kMetaFallback;
+    sl.m(0) = nk; sl.m(1) = ncp; sl.m(2) = g.npk; sl.m(3) = flags;
+}
+
+__device__ void team_a3(const Slot& sl, int r, int TS) {
+    if (sl.m(3) & kMetaFallback) return;
+    const int n = sl.m(0);
+    for (int i = r; i < n; i += TS) {
+        double lo = 0, dg, up = 0, rr;
+        if (i == 0) { dg = 2.0; up = 0.0; rr = 0.0; }
+        else if (i == n - 1) { dg = 2.0; lo = 0.0; rr = 0.0; }
+        else {
+            const double xm = sl.x(i - 1), x0 = sl.x(i), xp = sl.x(i + 1);
+            const double ym = sl.y(i - 1), y0 = sl.y(i), yp = sl.y(i + 1);
+            lo = 1.0 / 3.0 * (x0 - xm);
+            dg = 2.0 / 3.0 * (xp - xm);
+            up = 1.0 / 3.0 * (xp - x0);
+            rr = (yp - y0) / (xp - x0) - (y0 - ym) / (x0 - xm);
+        }
+        const double sd = 1.0 / dg;                                     // saved_diag
+        sl.a(i) = up * sd; sl.c(i) = lo * sd; sl.b(i) = rr * sd;
+    }
+}
+
+__device__ void team_a4(const Slot& sl) {
+    if (sl.m(3) & kMetaFallback) return;
+    const int n = sl.m(0);
+    double up_prev = 0, dg_prev = 1, yy_prev = 0;
+    for (int i = 0; i < n; i++) {
+        double lo = sl.c(i);
+        const double up = sl.a(i);
+        double dg = 1.0;
+        double sum = 0;
+        if (i > 0) {
+            const double xx = -lo / dg_prev;                            // Gauss step k = i-1
+            lo = -xx;
+            dg = dg + xx * up_prev;
+            sum += lo * yy_prev;                                        // l_solve
+        }
+        const double yy = sl.b(i) - sum;
+        sl.c(i) = dg; sl.b(i) = yy;
+        up_prev = up; dg_prev = dg; yy_prev = yy;
+    }
+    double bb_next = 0;
+    for (int i = n - 1; i >= 0; i--) {                                  // r_solve
+        double sum = 0;
+        if (i < n - 1) sum += sl.a(i) * bb_next;
+        const double bb = (sl.b(i) - sum) / sl.c(i);
+        sl.b(i) = bb;
+        bb_next = bb;
+    }
+}
+
+__device__ void team_a5(const Slot& sl, int r, int TS) {
+    if (sl.m(3) & kMetaFallback) return;
+    const int n = sl.m(0);
+    for (int i = r; i < n - 1; i += TS) {                               // spline.h:345-349
+        const double dx = sl.x(i + 1) - sl.x(i);
+        const double a = 1.0 / 3.0 * (sl.b(i + 1) - sl.b(i)) / dx;
+        const double c = (sl.y(i + 1) - sl.y(i)) / dx - 1.0 / 3.0 * (2.0 * sl.b(i) + sl.b(i + 1)) * dx;
+        sl.a(i) = a; sl.c(i) = c;
+        if (i == n - 2) {                                               // spline.h:367-370
+            const double h = sl.x(n - 1) - sl.x(n - 2);
+            sl.a(n - 1) = 0.0;
+            sl.c(n - 1) = 3.0 * a * h * h + 2.0 * sl.b(n - 2) * h + c;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Phase B: the resampling loop of one candidate (src/main.cpp:845-1041)
 // ------------------------------------------------------------------------------------------------
 struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj[2]; };
@@ -547,19 +723,50 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #else
     double prev_angle = 0;
 #endif
+#if PP_DIV_RCP & 4
+    double rtt = ppm::rcp_nr(sc.ttime);
+#define PP_SC_SPEED(t) sc_get_speed_r(sc, t, rtt)
+#else
+#define PP_SC_SPEED(t) sc_get_speed(sc, t)
+#endif
+#if PP_DIV_RCP & 2
+#define PP_DIV50(v) ppm::div_rcp(v, 50.0, 0.02)
+#else
+#define PP_DIV50(v) ((v) / 50)
+#endif
     while (arg < 50 && ng < room) {
-        double speed = sc_get_speed(sc, cur_t);
-        double dstep = speed / 50;
+        double speed = PP_SC_SPEED(cur_t);
+        double dstep = PP_DIV50(speed);
         const double x = arg + dstep;
         // tk::spline::operator() (spline.h:375-396)
-        if (!kCache || !(seg_lo < x && x <= seg_hi)) {
+#if PP_SEG_MODE == 2
+        // no cache: x never decreases along the walk (sp_step >= 0), so the lower_bound position
+        // only moves forward; the segment's coefficients are re-read from LDS every step
+        (void)seg_lo; (void)seg_hi;
+        while (cnt < nk && sl.x(cnt) < x) cnt++;
+        {
+            const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+            sx = sl.x(idx); sa_ = sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+        }
+#else
+        if (!kCache || !(seg_lo < x && x <= seg_hi)
+#if PP_SEG_MODE == 9      // diagnostic timing build: the first step's segment for the whole walk
+            && ng == 0
+#endif
+        ) {
+#if PP_SEG_MODE == 1      // forward only unless x fell below the cached segment
+            if (__builtin_expect(x <= seg_lo, 0)) while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
+            else while (cnt < nk && sl.x(cnt) < x) cnt++;
+#else
             while (cnt < nk && sl.x(cnt) < x) cnt++;
             while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
+#endif
             const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
             seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
             seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
             sx = sl.x(idx); sa_ = sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
         }
+#endif
         const double h = x - sx;
         double y;
         if (cnt == 0 && x < sx) y = (sb * h + sc_) * h + sy;                       // left
@@ -571,10 +778,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
         // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
         double ux, uy;
+        const double rd = ppm::rcp_nr(d);
         {
             const double ddx = x - pos_x, ddy = y - pos_y;
-            const double r = ppm::rcp_nr(d);
-            ux = ddx * r; uy = ddy * r;
+            ux = ddx * rd; uy = ddy * rd;
             if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
@@ -596,7 +803,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 sc_override(sc, cur_t, ns);
                 speed = ns;
                 sc.ttime += 0.02;
-                dstep = speed / 50;
+#if PP_DIV_RCP & 4
+                rtt = ppm::rcp_nr(sc.ttime);
+#endif
+                dstep = PP_DIV50(speed);
                 acc = na;
                 R.flags |= PP_ST_ACC_OVERRIDE;
             }
@@ -638,8 +848,13 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #else
         prev_angle = astep;
 #endif
+#if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
+        const double sp_step = ppm::div_rcp((x - pos_x) * dstep, d, rd);
+        pos_y += ppm::div_rcp((y - pos_y) * dstep, d, rd);
+#else
         const double sp_step = (x - pos_x) * dstep / d;
         pos_y += (y - pos_y) * dstep / d;
+#endif
         arg += sp_step;
         pos_x += sp_step;
         if (kOutMode != 0 && kOut) {
@@ -735,11 +950,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         if (!__syncthreads_or(mine)) return;
     }
     if (tid < SPB) sFlags[tid] = 0;
+#if PP_TEAM_SETUP
+    {   // phase A: a team of TS threads per slot (team_a1..a5), block barriers between the steps
+        int TS = (int)blockDim.x / nslot;
+        if (TS > 8) TS = 8;
+        const int j = tid / TS, r = tid - j * TS;
+        const bool act = j < NL * nsc && (((pv.lim_mask[(s0 + j / NL) * D] & kLimSlow) != 0) == kSlow);
+        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
+        const int L = j % NL;
+        const int64_t s = s0 + j / NL;
+        LaneGeom g;
+        if (act) { g = lane_geom(pv, s * D, Sv, L); team_a1(m, in, g, s, L, sl, r, TS); }
+        __syncthreads();
+        if (act && r == 0) team_a2(g, sl);
+        __syncthreads();
+        if (act) team_a3(sl, r, TS);
+        __syncthreads();
+        if (act && r == 0) team_a4(sl);
+        __syncthreads();
+        if (act) team_a5(sl, r, TS);
+    }
+#else
     if (tid < NL * nsc && (((pv.lim_mask[(s0 + tid / NL) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
         const int j = tid;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         setup_lane(m, P, in, pv, s0 + j / NL, (s0 + j / NL) * D, Sv, j % NL, sl);
     }
+#endif
     __syncthreads();
 #ifdef PP_ABL_NO_PHASE_B   // diagnostic timing build: phase A only
     if (tid < nsc) out.status[s0 + tid] = 0;

@@ -268,6 +268,21 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return r;
 }
 
+// n / d from r ~ 1/d (within ~1 ulp): q0 = n r, then one Markstein correction with the exact
+// residual n - q0 d (fma). With r within half an ulp of 1/d (r = RN(1/d), e.g. 0.02 for 50) the
+// result is the correctly rounded quotient; with rcp_nr's r it is in all but rare cases (then one
+// ulp away). Zero and non-finite operands, and |d| or |n| outside [2^-900, 2^900] (where the
+// residual could underflow), take the IEEE division.
+__device__ __forceinline__ double div_rcp(double n, double d, double r) {
+    const double q0 = n * r;
+    const double e = __builtin_fma(-q0, d, n);
+    const double q = __builtin_fma(e, r, q0);
+    const double ad = fabs(d), an = fabs(n);
+    const bool ok = ad >= 0x1p-900 && ad <= 0x1p900 && (an == 0.0 || (an >= 0x1p-900 && an <= 0x1p900));
+    if (__builtin_expect(!ok, 0)) return n / d;
+    return an == 0.0 ? q0 : q;        // +-0 / d: q0 carries the quotient's sign
+}
+
 // fmod(a, 2*pi) for the reference's angle wrap fmod(d + 3*pi, 2*pi) - pi
 // (src/main.cpp:870, 934). fmod is exact, so any exact evaluation is bit-identical: for
 // 0 <= a < 3*(2*pi) the remainder a - k*(2*pi), k in {0, 1, 2}, is computed exactly
