@@ -49,6 +49,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
     return m;
 }
 
+#ifndef PP_EMIT_ROTATE
+#define PP_EMIT_ROTATE 1
+#endif
 #ifndef PP_TEAM_SETUP
 #define PP_TEAM_SETUP 1
 #endif
@@ -64,7 +67,7 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #define PP_DIV_RCP 7
 #endif
 #ifndef PP_PREP_WAVES
-#define PP_PREP_WAVES 3
+#define PP_PREP_WAVES 4
 #endif
 // kLdsMap: the map (kMapArrays n doubles) is staged in LDS (n <= kLdsMapMax: <= 62.4 KB, 600
 // waypoints at three lanes); larger maps are read from global memory (L2-resident) by the same code.
@@ -1161,6 +1164,35 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
     double ca = pv.ca_p[s], sa = pv.sa_p[s];
     const uint64_t m0 = adjm[s], m1 = adjm[S + s];
     double pxp = 0, pyp = 0;                       // local position before the step
+#if PP_EMIT_ROTATE
+    // The adjusted steps are sparse and scattered over the wave's lanes, so the rotation block
+    // runs, with few lanes active, on most steps: it is kept short. The heading's sin/cos follow
+    // by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead of sin/cos of the
+    // accumulated angle (src/main.cpp:996-997): equal to ~1 ulp per adjustment.
+    for (int g = 0; g < ng; g++) {
+        const bool bit = (g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0;
+        if (bit) {
+            const double rot = rec[2 * rstride + (int64_t)g * S + s];
+            double cr, sr;
+            ppm::sincos_pp<true>(rot, sr, cr);
+            const double tpx = (pxp * ca - pyp * sa) + cx;
+            const double tpy = (pxp * sa + pyp * ca) + cy;
+            const double vx = cx - tpx, vy = cy - tpy;
+            cx = tpx + (vx * cr - vy * sr);
+            cy = tpy + (vx * sr + vy * cr);
+            const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
+            ca = nca; sa = nsa;
+        }
+        const double px_ = rec[(int64_t)g * S + s], py_ = rec[rstride + (int64_t)g * S + s];
+        const double tx = px_ * ca - py_ * sa;
+        const double ty = px_ * sa + py_ * ca;
+        out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
+        out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+        pxp = px_;
+        pyp = py_;
+    }
+    (void)tangle;
+#else
     for (int g = 0; g < ng; g++) {
         const uint64_t bit = g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1;
         if (bit) {
@@ -1187,6 +1219,7 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
         pxp = px_;
         pyp = py_;
     }
+#endif
     for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
 }
 

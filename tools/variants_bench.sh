@@ -2,6 +2,7 @@
 # On the GPU box: times every libppamd_var_*.so (and the product library) with bench.py, one
 # process after another; one summary line per library into gpurun_out/variants.txt.
 cd "$(dirname "$0")/.." || exit 1
+shopt -s nullglob
 mkdir -p gpurun_out
 out=gpurun_out/variants.txt
 : > $out
