@@ -49,6 +49,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
     return m;
 }
 
+#ifndef PP_STEP_FAST
+#define PP_STEP_FAST 1
+#endif
 #ifndef PP_EMIT_ROTATE
 #define PP_EMIT_ROTATE 1
 #endif
@@ -775,23 +778,40 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         if (cnt == 0 && x < sx) y = (sb * h + sc_) * h + sy;                       // left
         else if (cnt == nk && x > sx) y = (sb * h + sc_) * h + sy;                 // right
         else y = ((sa_ * h + sb) * h + sc_) * h + sy;
+#if PP_STEP_FAST
+        double d, rd;
+        const bool dok = ppm::sqrt_rd((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y), d, rd);
+#else
         const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
+#endif
         double acc = fabs(speed - prev_speed) * 50;
 #if PP_ANGLE_CROSS
         // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
         // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
         double ux, uy;
+#if !PP_STEP_FAST
         const double rd = ppm::rcp_nr(d);
+#endif
         {
             const double ddx = x - pos_x, ddy = y - pos_y;
             ux = ddx * rd; uy = ddy * rd;
             if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
+#if PP_STEP_FAST
+        // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
+        // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
+        double adiff;
+        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1))
+            adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
+        else
+            adiff = ppm::fmod_2pi(ppm::atan2_fast(cr, dt) + 3 * kPi) - kPi;
+#else
         double adt;
         if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1)) adt = ppm::asin_small(cr);
         else adt = ppm::atan2_fast(cr, dt);
         const double adiff = ppm::fmod_2pi(adt + 3 * kPi) - kPi;
+#endif
 #else
         const double astep = ppm::atan2_fast(y - pos_y, x - pos_x);
         const double adiff = ppm::fmod_2pi(astep - prev_angle + 3 * kPi) - kPi;
@@ -851,7 +871,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #else
         prev_angle = astep;
 #endif
-#if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
+#if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS && PP_STEP_FAST
+        const double sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
+        pos_y += ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok);
+#elif (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
         const double sp_step = ppm::div_rcp((x - pos_x) * dstep, d, rd);
         pos_y += ppm::div_rcp((y - pos_y) * dstep, d, rd);
 #else

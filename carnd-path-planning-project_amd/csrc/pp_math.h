@@ -283,6 +283,41 @@ __device__ __forceinline__ double div_rcp(double n, double d, double r) {
     return an == 0.0 ? q0 : q;        // +-0 / d: q0 carries the quotient's sign
 }
 
+// n / d with r ~ 1/d for a d known to lie in [2^-450, 2^450] (dok: sqrt_rd's fast path);
+// otherwise, and for |n| outside [2^-900, 2^900], the IEEE division
+__device__ __forceinline__ double div_rcp_n(double n, double d, double r, bool dok) {
+    const double q0 = n * r;
+    const double e = __builtin_fma(-q0, d, n);
+    const double q = __builtin_fma(e, r, q0);
+    const double an = fabs(n);
+    if (__builtin_expect(!(dok && an >= 0x1p-900 && an <= 0x1p900), 0)) return (dok && an == 0.0) ? q0 : n / d;
+    return q;
+}
+
+// d = sqrt(q) correctly rounded and rd ~ 1/d; returns whether q was in [2^-900, 2^900]. There
+// this is the ISA sequence the compiler emits for an IEEE sqrt (v_rsq_f64, then Goldschmidt
+// g ~ sqrt(q), h ~ 1/(2 sqrt(q)) and two residual corrections of g), without its range scaling
+// and 0/inf fix-ups, and rd = 2 h. Elsewhere (0, tiny, huge, inf, NaN): sqrt and 1 / d.
+__device__ __forceinline__ bool sqrt_rd(double q, double& d, double& rd) {
+    if (__builtin_expect(q >= 0x1p-900 && q <= 0x1p900, 1)) {
+        const double y0 = __builtin_amdgcn_rsq(q);
+        double g = q * y0;
+        double h = 0.5 * y0;
+        const double e = __builtin_fma(-h, g, 0.5);
+        g = __builtin_fma(g, e, g);
+        h = __builtin_fma(h, e, h);
+        const double d0 = __builtin_fma(-g, g, q);
+        g = __builtin_fma(d0, h, g);
+        const double d1 = __builtin_fma(-g, g, q);
+        d = __builtin_fma(d1, h, g);
+        rd = 2.0 * h;
+        return true;
+    }
+    d = __builtin_sqrt(q);
+    rd = 1.0 / d;
+    return false;
+}
+
 // fmod(a, 2*pi) for the reference's angle wrap fmod(d + 3*pi, 2*pi) - pi
 // (src/main.cpp:870, 934). fmod is exact, so any exact evaluation is bit-identical: for
 // 0 <= a < 3*(2*pi) the remainder a - k*(2*pi), k in {0, 1, 2}, is computed exactly
