@@ -185,6 +185,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
                 cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
             }
             int nwp = 0;
+#ifdef PP_ABL_SKIP_FAR   // diagnostic timing build: cars beyond PP_ABL_SKIP_FAR metres skipped
+            if ((cx - ego_x) * (cx - ego_x) + (cy - ego_y) * (cy - ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
+#endif
             if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;

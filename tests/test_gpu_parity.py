@@ -141,6 +141,25 @@ def test_random_scenes_vs_oracle(env, mode):
     print(f"random mode={mode}: max |dxy| {e:.3e} m")
 
 
+def test_tied_cars_vs_oracle(env):
+    """Cars duplicated under later ids (identical position and velocity): the running minima of
+    the planner and of the follow-car choice keep the earlier id, as the reference's id-order
+    pass does, although k_prep visits the cars nearest class first."""
+    S = 2000
+    sc = ppamd.synth_host(env["m"], S, seed=77, first=4242)
+    for j in range(6, 12):
+        for k in ("car_x", "car_y", "car_vx", "car_vy"):
+            sc[k][j] = sc[k][j - 6]
+    prm = ppamd.default_params(emit_paths=True)
+    got = run_gpu(env, to_dev(env, sc), prm, info=True)
+    ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=True)
+    compare(got, ref)
+    for k in ("in_lane_car", "target_lane", "lane_open_mask", "n_matched_cars", "ego_lane"):
+        assert np.array_equal(got["info"][k], ref["info"][k]), k
+    np.testing.assert_allclose(got["info"]["lane_score"], ref["info"]["lane_score"], rtol=0, atol=1e-12)
+    assert (got["info"]["in_lane_car"] >= 0).sum() > S // 4
+
+
 def test_device_synth_matches_host_synth(env):
     dev = ppamd.scenes_to_numpy(ppamd.synth_device(env["m"], 2000, seed=31, first=777, device=0))
     host = ppamd.synth_host(env["m"], 2000, seed=31, first=777)
