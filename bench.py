@@ -53,9 +53,10 @@ def load_valu_peak():
     """Measured FP64 VALU issue rate (tools/valu_peak.hip on the MI355X, profiles/r01_valu_peak.json)."""
     p = os.path.join(REPO, "profiles", "r01_valu_peak.json")
     try:
-        return json.load(open(p))["v_fma_f64"]["wave_instr_per_s"]
+        j = json.load(open(p))
+        return j["v_fma_f64"]["wave_instr_per_s"], j["v_add_f64"]["wave_instr_per_s"]
     except Exception:
-        return None
+        return None, None
 
 
 def load_f64_instr(tag):
@@ -234,7 +235,7 @@ def main():
     }
     # the bound that matters for this path: FP64 VALU issue (no MFMA-shaped work, HBM ~3 %)
     f64, allv = load_f64_instr(tag)
-    peak = load_valu_peak()
+    peak, peak_add = load_valu_peak()
     if f64 and peak:
         ach = f64 / (k_cand_ms * 1e-3)
         out["valu_roofline"] = {"bound": "fp64-valu-issue", "kernel": "k_cand",
@@ -243,6 +244,12 @@ def main():
                                 "f64_wave_instr_per_launch": f64,
                                 "source": "rocprofv3 PMC SQ_INSTS_VALU_*_F64 per launch (profiles/pmc_summary.json) "
                                           "/ this run's k_cand time; peak measured by tools/valu_peak.hip"}
+        if allv and peak_add:
+            # every VALU instruction (FP64, int, moves, compares) against the fastest measured
+            # single-instruction issue rate (v_add_f64): the share of the VALU issue slots used
+            out["valu_roofline"]["all_valu_wave_instr_per_s"] = allv / (k_cand_ms * 1e-3)
+            out["valu_roofline"]["peak_issue_wave_instr_per_s"] = peak_add
+            out["valu_roofline"]["issue_frac"] = allv / (k_cand_ms * 1e-3) / peak_add
     if a.rollout:
         out["scene_frames_per_s"] = S * world * a.steps * frames / elapsed
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
