@@ -297,6 +297,13 @@ __device__ __forceinline__ void sc_override(SC& c, double t, double speed) {
     const double mt = c.ttime * (speed - c.start) / (c.target - c.start);
     c.shift = t - mt;
 }
+// sc_override with r ~ 1 / (target - start) (ppm::div_rcp): the same quotient
+__device__ __forceinline__ void sc_override_r(SC& c, double t, double speed, double r) {
+    if (t > c.ttime) return;
+    if (fabs(c.target - c.start) < kEps) return;
+    const double mt = ppm::div_rcp(c.ttime * (speed - c.start), c.target - c.start, r);
+    c.shift = t - mt;
+}
 
 // LimitSpeed::calculate (src/main.cpp:1068-1150). Returns 0 FREEFLOW 1 BRAKE 2 MAXBRAKE 3 ADJUST 4 KEEP.
 __device__ inline int limit_speed(const pp_params& P, double fvx, double fvy, double next_s,

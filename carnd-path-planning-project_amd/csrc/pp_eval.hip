@@ -66,8 +66,13 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #endif
 // Divisions of the candidate loop as a reciprocal and one correction step (ppm::div_rcp):
 // bit 0: the two divisions by the step length d, bit 1: speed / 50, bit 2: the speed ramp / ttime
+// (bit 2 is off: keeping 1/ttime current through the overrides costs more than it saves)
 #ifndef PP_DIV_RCP
-#define PP_DIV_RCP 7
+#define PP_DIV_RCP 3
+#endif
+// the override's divisions (na / 50 and SpeedController::override_speed) by reciprocals
+#ifndef PP_OVR_RCP
+#define PP_OVR_RCP 1
 #endif
 #ifndef PP_PREP_WAVES
 #define PP_PREP_WAVES 4
@@ -732,6 +737,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #else
     double prev_angle = 0;
 #endif
+#if PP_OVR_RCP
+    // 1 / (target - start) for SpeedController::override_speed (constant over the walk)
+    const double rds = ppm::rcp_nr(sc.target - sc.start);
+#endif
 #if PP_DIV_RCP & 4
     double rtt = ppm::rcp_nr(sc.ttime);
 #define PP_SC_SPEED(t) sc_get_speed_r(sc, t, rtt)
@@ -805,7 +814,11 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
         double adiff;
+#ifdef PP_ABL_NO_WIDE      // diagnostic timing build: every turn through the series
+        if (true)
+#else
         if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1))
+#endif
             adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
         else
             adiff = ppm::fmod_2pi(ppm::atan2_fast(cr, dt) + 3 * kPi) - kPi;
@@ -821,12 +834,25 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
+#ifdef PP_ABL_NO_LIMITER   // diagnostic timing build: the limiter branch never runs
+        if (false) {
+#else
         if (acc + cacc > P.maximum_acc) {
+#endif
+#ifdef PP_ABL_NO_OVERRIDE  // diagnostic timing build: the speed override never runs
+            if (false) {
+#else
             if (speed > prev_speed) {                                   // :945-971
+#endif
                 double na = P.maximum_acc - cacc;
                 if (na < 0) na = 0;
+#if PP_OVR_RCP
+                const double ns = prev_speed + PP_DIV50(na);
+                sc_override_r(sc, cur_t, ns, rds);
+#else
                 const double ns = prev_speed + na / 50;
                 sc_override(sc, cur_t, ns);
+#endif
                 speed = ns;
                 sc.ttime += 0.02;
 #if PP_DIV_RCP & 4
