@@ -239,6 +239,50 @@ __device__ inline void get_lane_pos_multi(const MapV& m, int ref_wp, double rati
         if ((pending >> i) & 1) { ox[i] = nx_ * 0.0 + px_ * (1 - 0.0); oy[i] = ny_ * 0.0 + py_ * (1 - 0.0); }
 }
 
+// Map::get_lane_pos for a target s > 0: the walk only moves forward (s stays > 0, :291-302). The
+// first kPf segments' lane-centre points and lengths are loaded up front, so their global-memory
+// latencies overlap instead of chaining one per step; same arithmetic, same result.
+template <int kPf>
+__device__ inline void get_lane_pos_fwd(const MapV& m, int ref_wp, double ratio, double s, int lane,
+                                        double& ox, double& oy, bool& ok) {
+    const int n = m.n;
+    const double* cx = m.lc_x + lane * n;
+    const double* cy = m.lc_y + lane * n;
+    const double* cl = m.llen + lane * n;
+    double qx[kPf + 1], qy[kPf + 1], ql[kPf + 1];
+#pragma unroll
+    for (int k = 0; k <= kPf; k++) {
+        const int b = wpi(ref_wp - 1 + k, n);
+        qx[k] = cx[b]; qy[k] = cy[b]; ql[k] = cl[b];
+    }
+    ok = false;
+    double dest = 0, nx_ = 0, ny_ = 0, px_ = 0, py_ = 0;
+#pragma unroll
+    for (int k = 0; k < kPf; k++) {
+        nx_ = qx[k + 1]; ny_ = qy[k + 1]; px_ = qx[k]; py_ = qy[k];
+        const double wl = ql[k + 1];
+        const double rem = wl * (1 - ratio);
+        if (s <= rem) { dest = 1 - (rem - s) / wl; ok = true; break; }
+        s -= rem;
+        ratio = 0;
+    }
+    if (!ok) {
+        int wp = ref_wp + kPf;
+        for (int it = kPf; it < 4 * n + 8; it++) {
+            const int b = wpi(wp, n), a = wpi(wp - 1, n);
+            nx_ = cx[b]; ny_ = cy[b]; px_ = cx[a]; py_ = cy[a];
+            const double wl = cl[b];
+            const double rem = wl * (1 - ratio);
+            if (s <= rem) { dest = 1 - (rem - s) / wl; ok = true; break; }
+            s -= rem;
+            ratio = 0;
+            wp++;
+        }
+    }
+    ox = nx_ * dest + px_ * (1 - dest);
+    oy = ny_ * dest + py_ * (1 - dest);
+}
+
 // Map::get_lane_pos (src/main.cpp:277-328) on one lane. ok=false if the bounded walk ran out.
 __device__ inline void get_lane_pos(const MapV& m, int ref_wp, double ratio, double s, int lane,
                                     double& ox, double& oy, bool& ok) {

@@ -30,6 +30,22 @@
 
 using namespace ppd;
 
+#ifdef PP_DIAG
+// diagnostic builds only (-DPP_DIAG): per event, [2k] lanes where it fired, [2k+1] waves where any
+// lane fired (the wave executes the branch). Read with pp_diag_read.
+__device__ unsigned long long g_diag[32];
+__device__ __forceinline__ void diag(int k, bool c) {
+    const unsigned long long b = __ballot(c);
+    if (b && __lane_id() == (unsigned)__builtin_ctzll(__ballot(1))) {
+        atomicAdd(&g_diag[2 * k], (unsigned long long)__builtin_popcountll(b));
+        atomicAdd(&g_diag[2 * k + 1], 1ull);
+    }
+}
+#define PP_DIAGC(k, c) diag(k, c)
+#else
+#define PP_DIAGC(k, c) ((void)0)
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
@@ -60,6 +76,14 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #endif
 #ifndef PP_SEG_MODE
 #define PP_SEG_MODE 0
+#endif
+// segments of the control-point walk loaded ahead (get_lane_pos_fwd)
+#ifndef PP_WALK_PF
+#define PP_WALK_PF 4
+#endif
+// phase A's serial steps (control-point distance rule, band sweeps) on the block's first wave
+#ifndef PP_SERIAL_WAVE
+#define PP_SERIAL_WAVE 1
 #endif
 #ifndef PP_ANGLE_CROSS
 #define PP_ANGLE_CROSS 1
@@ -561,7 +585,12 @@ __device__ void team_a1(const MapV& m, const pp_scene_batch& in, const LaneGeom&
         for (int i = 1; i <= k; i++) cps = cps + g.min_cpd;
         double px, py;
         bool ok;
-        get_lane_pos(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
+#if defined(PP_ABL_A) && (PP_ABL_A & 1)   // diagnostic timing build: no map walk
+        px = g.pos_x + cps; py = g.pos_y + 0.01 * cps * cps; ok = true; (void)m;
+#else
+        if (cps > 0) get_lane_pos_fwd<PP_WALK_PF>(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
+        else get_lane_pos(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
+#endif
         const int j = g.npk + 1 + k;
         sl.a(j) = px; sl.b(j) = py; sl.c(j) = ok ? 1.0 : 0.0;
         const double tx0 = px - g.pos_x, ty0 = py - g.pos_y;
@@ -592,21 +621,30 @@ __device__ void team_a2(const LaneGeom& g, const Slot& sl) {
     sl.m(0) = nk; sl.m(1) = ncp; sl.m(2) = g.npk; sl.m(3) = flags;
 }
 
+// Each team lane takes a contiguous run of rows, so the slope (y(i+1) - y(i)) / (x(i+1) - x(i))
+// that row i's right-hand side shares with row i+1 is divided once per run, not twice.
 __device__ void team_a3(const Slot& sl, int r, int TS) {
     if (sl.m(3) & kMetaFallback) return;
     const int n = sl.m(0);
-    for (int i = r; i < n; i += TS) {
+    const int per = (n + TS - 1) / TS;
+    const int i0 = r * per, i1 = i0 + per < n ? i0 + per : n;
+    double sl_prev = 0;                                                 // slope of segment i-1
+    if (i0 > 0 && i0 < n - 1) sl_prev = (sl.y(i0) - sl.y(i0 - 1)) / (sl.x(i0) - sl.x(i0 - 1));
+    for (int i = i0; i < i1; i++) {
         double lo = 0, dg, up = 0, rr;
         if (i == 0) { dg = 2.0; up = 0.0; rr = 0.0; }
         else if (i == n - 1) { dg = 2.0; lo = 0.0; rr = 0.0; }
         else {
             const double xm = sl.x(i - 1), x0 = sl.x(i), xp = sl.x(i + 1);
-            const double ym = sl.y(i - 1), y0 = sl.y(i), yp = sl.y(i + 1);
+            const double y0 = sl.y(i), yp = sl.y(i + 1);
             lo = 1.0 / 3.0 * (x0 - xm);
             dg = 2.0 / 3.0 * (xp - xm);
             up = 1.0 / 3.0 * (xp - x0);
-            rr = (yp - y0) / (xp - x0) - (y0 - ym) / (x0 - xm);
+            const double sl_i = (yp - y0) / (xp - x0);
+            rr = sl_i - sl_prev;                // (yp - y0)/(xp - x0) - (y0 - ym)/(x0 - xm)
+            sl_prev = sl_i;
         }
+        if (i == 0 && n > 2) sl_prev = (sl.y(1) - sl.y(0)) / (sl.x(1) - sl.x(0));
         const double sd = 1.0 / dg;                                     // saved_diag
         sl.a(i) = up * sd; sl.c(i) = lo * sd; sl.b(i) = rr * sd;
     }
@@ -677,7 +715,8 @@ template <bool kLarge, int kOutMode, bool kCache>
 __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
                                  double angle, double ca0, double sa0, SC sc, int room, double* wx,
                                  double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true,
-                                 double* rec = nullptr) {
+                                 double* rec = nullptr, int dcls = 0) {
+    (void)dcls;   // PP_DIAG builds: candidate class (|L - ego lane|) for the census
     const bool kOut = kOutMode == 2 || (kOutMode == 1 && out_on);
     const bool kRec = kOutMode == 3 && out_on;
     const int64_t rstride = (int64_t)room * ws;
@@ -753,6 +792,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #define PP_DIV50(v) ((v) / 50)
 #endif
     while (arg < 50 && ng < room) {
+        PP_DIAGC(0, true);
+        PP_DIAGC(2, !(s_max(cur_t - sc.shift, 0.0) > sc.ttime));
         double speed = PP_SC_SPEED(cur_t);
         double dstep = PP_DIV50(speed);
         const double x = arg + dstep;
@@ -779,6 +820,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             while (cnt < nk && sl.x(cnt) < x) cnt++;
             while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
 #endif
+            PP_DIAGC(1, true);
             const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
             seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
             seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
@@ -814,6 +856,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
         double adiff;
+        PP_DIAGC(3, !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
+        PP_DIAGC(8, ng == 0 && !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
+        PP_DIAGC(9, !(dt > 0));
 #ifdef PP_ABL_NO_WIDE      // diagnostic timing build: every turn through the series
         if (true)
 #else
@@ -834,6 +879,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
+        PP_DIAGC(4, acc + cacc > P.maximum_acc);
+        PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
+        PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
+        PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
 #ifdef PP_ABL_NO_LIMITER   // diagnostic timing build: the limiter branch never runs
         if (false) {
 #else
@@ -862,6 +911,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 acc = na;
                 R.flags |= PP_ST_ACC_OVERRIDE;
             }
+            PP_DIAGC(6, acc + cacc > P.maximum_acc);
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
                 double nc = P.maximum_acc - acc;
                 if (nc < 0) nc = 0;
@@ -1017,13 +1067,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         LaneGeom g;
         if (act) { g = lane_geom(pv, s * D, Sv, L); team_a1(m, in, g, s, L, sl, r, TS); }
         __syncthreads();
+#if PP_SERIAL_WAVE
+        // the two serial steps (A2, A4) on one lane per slot, slots in lane order: NL * SPB <= 64
+        // slots fit the block's first wave, whose instruction stream is then the only one paying
+        // for them (a team layout spreads them over every wave of the block)
+        const int js = tid;
+        const bool act_s = js < NL * nsc && (((pv.lim_mask[(s0 + js / NL) * D] & kLimSlow) != 0) == kSlow);
+        const Slot sls = {sX + js * kKP, sY + js * kKP, sA + js * kKP, sB + js * kKP, sC + js * kKP, sMeta + 4 * js, 1};
+        if (act_s) {
+            const int64_t vs = (s0 + js / NL) * D;
+            LaneGeom gs;
+            gs.K = pv.K[vs];
+            gs.npk = gs.K > 0 ? gs.K - 1 : 0;
+            gs.pos_x = pv.pos_x[vs]; gs.pos_y = pv.pos_y[vs]; gs.ego_d = pv.ego_d[vs];
+            team_a2(gs, sls);
+        }
+#else
         if (act && r == 0) team_a2(g, sl);
+#endif
         __syncthreads();
-        if (act) team_a3(sl, r, TS);
+#ifndef PP_ABL_A
+#define PP_ABL_A 0
+#endif
+        if (!(PP_ABL_A & 4) && act) team_a3(sl, r, TS);   // PP_ABL_A: diagnostic timing builds
         __syncthreads();
-        if (act && r == 0) team_a4(sl);
+#if PP_SERIAL_WAVE
+        if (!(PP_ABL_A & 2) && act_s) team_a4(sls);
+#else
+        if (!(PP_ABL_A & 2) && act && r == 0) team_a4(sl);
+#endif
         __syncthreads();
-        if (act) team_a5(sl, r, TS);
+        if (!(PP_ABL_A & 4) && act) team_a5(sl, r, TS);
     }
 #else
     if (tid < NL * nsc && (((pv.lim_mask[(s0 + tid / NL) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
@@ -1115,7 +1189,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
             }
         } else {
             R = run_candidate<kSlow, 0, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
-                                                       nullptr, nullptr, 0, nullptr, 0);
+                                                       nullptr, nullptr, 0, nullptr, 0, true, nullptr,
+                                                       fabs(sc.target - sc.start) >= 7.5 * sc.ttime ? 2 : (sc.target > sc.start ? 1 : 0));
         }
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * Sv + v], L, T, vt, pv.open_mask[v],
@@ -1692,6 +1767,16 @@ double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int3
     return ppsynth::mc_gauss(seed, (uint64_t)scene, draw, car, q);
 }
 
+#ifdef PP_DIAG
+int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic builds only
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 const char* pp_version(void) { return "pp-mi355x 0.1 (gfx950, fp64, lane-per-candidate)"; }
 
 int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out) {
