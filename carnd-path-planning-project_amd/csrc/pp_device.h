@@ -11,19 +11,28 @@
 #include "../../include/pp.h"
 #include "pp_math.h"
 
+#ifndef PP_DIAGC   // branch-event census hook (pp_eval.hip, PP_DIAG builds)
+#define PP_DIAGC(k, c) ((void)0)
+#endif
+
 namespace ppd {
 
 constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
 constexpr double kEps = 1e-5;                     // src/main.cpp:24
 constexpr int kKP = 17;                           // LDS knot stride (16 knots + 1 pad: bank spread)
 constexpr int NL = PP_NUM_LANES;                  // lanes (src/main.cpp:22)
-constexpr int kMapArrays = 4 + 3 * NL;            // ref x/y, normal x/y, lane centre x[NL]/y[NL], length[NL]
+// ref x/y, normal x/y, lane centre x[NL]/y[NL], length[NL], segment |.|^2 [NL] and its reciprocal [NL]
+constexpr int kMapArrays = 4 + 5 * NL;
 
 // Map geometry (SoA). Arrays [i] or [lane * n + i]. llen[lane*n+i] = |lc[i] - lc[i-1]|
 // (Map::get_lane_length, src/main.cpp:138-142), precomputed on the host with the same formula.
+// lden[lane*n+i] = (ax - bx)^2 + (ay - by)^2 for a = lc[i-1], b = lc[i]: distancesq_pt_seg's rdenom
+// (helpers.h:202) for that lane segment, and lrcp = RN(1 / lden). fastm: every lden lies in
+// [2^-500, 2^500] (no degenerate lane segment), so lane_matching may use the tables.
 struct MapV {
-    const double *ref_x, *ref_y, *nx, *ny, *lc_x, *lc_y, *llen;
+    const double *ref_x, *ref_y, *nx, *ny, *lc_x, *lc_y, *llen, *lden, *lrcp;
     int n;
+    int fastm;
 };
 
 // Per-scene preparation output of K1 (SoA, workspace).
@@ -118,6 +127,7 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
     int b_lane = 0, b_cur = 0;
     double b_rnom = 0, b_rdenom = 1, b_snom = 0, b_ss = 0, b_sr = 0;
     for (int it = 0; it < 4 * n + 8; it++) {
+        PP_DIAGC(16, true);
         bool improved = false;
         const int a = wpi(cur - 1, n), b = wpi(cur, n);
 #pragma unroll
@@ -172,6 +182,119 @@ __device__ inline bool lane_matching(const MapV& m, int ref_wp, const double rat
         out_next_wp = b_cur;
     }
     return found;
+}
+
+// n / d correctly rounded from r = RN(1/d) (Markstein: q0 = RN(n r) is within an ulp of n/d, the
+// residual n - q0 d is exact by fma, and RN(q0 + residual r) is RN(n/d)), for d in [2^-500, 2^500]
+// and n = 0 or |n| in [2^-400, 2^400] (the quotient stays normal; 4e8 random operands in these
+// ranges, many with near-all-ones divisor significands, agree with IEEE division bit for bit);
+// elsewhere the IEEE division.
+__device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
+    const double q0 = n * r;
+    const double q = __builtin_fma(__builtin_fma(-q0, d, n), r, q0);
+    const double an = fabs(n);
+    if (__builtin_expect(!((an >= 0x1p-400 && an <= 0x1p400) || an == 0.0), 0)) return n / d;
+    return an == 0.0 ? q0 : q;
+}
+
+// lane_matching on a map with fastm: the same walk, with each lane segment's rdenom and its
+// reciprocal from the tables (the division snom^2 / rdenom by div_by_rcp: the same correctly
+// rounded value), and the waypoint indices stepped instead of re-wrapped.
+__device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double ratio[NL], double x,
+                                         double y, double& out_s, double& out_d, int& out_lane,
+                                         int& out_next_wp) {
+    const int n = m.n;
+    int dir = 0;
+    bool stop = false;
+    int cur = ref_wp;
+    int a = wpi(cur - 1, n), b = wpi(cur, n);
+    double sum_s[NL], sr[NL];
+#pragma unroll
+    for (int l = 0; l < NL; l++) { sum_s[l] = 0; sr[l] = ratio[l]; }
+    double best = 1000 * 1000;
+    bool found = false;
+    int b_lane = 0, b_cur = 0, b_b = 0;
+    double b_rnom = 0, b_snom = 0, b_ss = 0, b_sr = 0;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        PP_DIAGC(16, true);
+        bool improved = false;
+#pragma unroll
+        for (int lane = 0; lane < NL; lane++) {
+            const double ax = m.lc_x[lane * n + a], ay = m.lc_y[lane * n + a];
+            const double bx = m.lc_x[lane * n + b], by = m.lc_y[lane * n + b];
+            const double den = m.lden[lane * n + b];
+            const double pdx = x - ax, dx = bx - ax;                    // helpers.h:203-207
+            const double pdy = y - ay, dy = by - ay;
+            const double rn = pdx * dx + pdy * dy;
+            const double snom = pdx * dy - pdy * dx;
+            double rnom, dsq;
+            if (rn < -1) { rnom = 0; dsq = pdx * pdx + pdy * pdy; }                            // :227-231
+            else if (rn > den) { rnom = den; dsq = (x - bx) * (x - bx) + (y - by) * (y - by); }   // :232-236
+            else { rnom = rn; dsq = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]); }
+            if (dsq < best) {
+                best = dsq;
+                improved = true;
+                found = true;
+                b_lane = lane;
+                b_cur = cur;
+                b_b = b;
+                b_rnom = rnom; b_snom = snom;
+                b_sr = sr[lane];
+                b_ss = sum_s[lane];
+            }
+            if (rnom == 0) {
+                if (dir == 1) stop = true;
+                dir = -1;
+            } else if (rnom == den) {
+                if (dir == -1) stop = true;
+                dir = 1;
+            } else {
+                stop = true;
+            }
+        }
+        if (!improved || stop) break;
+        double ll[NL];
+#pragma unroll
+        for (int l = 0; l < NL; l++) ll[l] = m.llen[l * n + b];
+        if (dir > 0) {
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] += (1 - sr[l]) * ll[l]; sr[l] = 0; }
+            cur++;
+            a = b;
+            b = b + 1 == n ? 0 : b + 1;
+        } else {
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] -= sr[l] * ll[l]; sr[l] = 1; }
+            cur--;
+            b = a;
+            a = a == 0 ? n - 1 : a - 1;
+        }
+        // below -n the reference's size_t wrap (src/main.cpp:134-137) is not a plain modulus
+        if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
+    }
+    if (found) {                                                   // :214-227, last improvement
+        const double b_rdenom = m.lden[b_lane * n + b_b];
+        const double rfs = b_rnom / b_rdenom;
+        const double r_mod = rfs - b_sr;
+        const double seg_len = m.llen[b_lane * n + b_b];
+        out_s = b_ss + seg_len * r_mod;
+        double d = sqrt(best);
+        if (b_snom < 0) d = -d;
+        out_d = d + lane_offset(b_lane);
+        out_lane = b_lane;
+        out_next_wp = b_cur;
+    }
+    return found;
+}
+
+__device__ __forceinline__ bool lane_match(const MapV& m, int ref_wp, const double ratio[NL], double x,
+                                           double y, double& out_s, double& out_d, int& out_lane,
+                                           int& out_next_wp) {
+#ifndef PP_MATCH_TAB
+#define PP_MATCH_TAB 1
+#endif
+    if (PP_MATCH_TAB && m.fastm) return lane_matching_tab(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
+    return lane_matching(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
 }
 
 // Map::project_speed (src/main.cpp:330-358)

@@ -24,16 +24,10 @@
 #include <vector>
 
 #include "../../include/pp.h"
-#include "pp_device.h"
-#include "pp_math.h"
-#include "pp_synth.h"
-
-using namespace ppd;
-
 #ifdef PP_DIAG
 // diagnostic builds only (-DPP_DIAG): per event, [2k] lanes where it fired, [2k+1] waves where any
 // lane fired (the wave executes the branch). Read with pp_diag_read.
-__device__ unsigned long long g_diag[32];
+__device__ unsigned long long g_diag[64];
 __device__ __forceinline__ void diag(int k, bool c) {
     const unsigned long long b = __ballot(c);
     if (b && __lane_id() == (unsigned)__builtin_ctzll(__ballot(1))) {
@@ -45,12 +39,18 @@ __device__ __forceinline__ void diag(int k, bool c) {
 #else
 #define PP_DIAGC(k, c) ((void)0)
 #endif
+#include "pp_device.h"
+#include "pp_math.h"
+#include "pp_synth.h"
+
+using namespace ppd;
+
 
 // ------------------------------------------------------------------------------------------------
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
-// kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL]
-struct MapG { const double* buf; int n; };
+// kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL] lden[NL] lrcp[NL]
+struct MapG { const double* buf; int n; int fastm; };
 
 // |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
 // <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
@@ -58,10 +58,11 @@ constexpr double kSlowAngle = 1.0e5;
 constexpr int kLimSlow = 1 << 7;   // internal bit in PrepV.lim_mask
 static_assert(NL <= 6, "lim_mask: bit 0 in-lane limit, bits 1..NL lane limits, bit 7 kLimSlow");
 
-__device__ __forceinline__ MapV map_view(const double* b, int n) {
+__device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) {
     MapV m;
     m.ref_x = b; m.ref_y = b + n; m.nx = b + 2 * n; m.ny = b + 3 * n;
-    m.lc_x = b + 4 * n; m.lc_y = b + (4 + NL) * n; m.llen = b + (4 + 2 * NL) * n; m.n = n;
+    m.lc_x = b + 4 * n; m.lc_y = b + (4 + NL) * n; m.llen = b + (4 + 2 * NL) * n;
+    m.lden = b + (4 + 3 * NL) * n; m.lrcp = b + (4 + 4 * NL) * n; m.n = n; m.fastm = fastm;
     return m;
 }
 
@@ -81,6 +82,10 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #ifndef PP_WALK_PF
 #define PP_WALK_PF 4
 #endif
+// k_prep visits the cars nearest first (ties by iteration index keep the reference's results)
+#ifndef PP_CAR_SORT
+#define PP_CAR_SORT 1
+#endif
 // phase A's serial steps (control-point distance rule, band sweeps) on the block's first wave
 #ifndef PP_SERIAL_WAVE
 #define PP_SERIAL_WAVE 1
@@ -99,11 +104,25 @@ __device__ __forceinline__ MapV map_view(const double* b, int n) {
 #define PP_OVR_RCP 1
 #endif
 #ifndef PP_PREP_WAVES
-#define PP_PREP_WAVES 4
+#define PP_PREP_WAVES 3
 #endif
 // kLdsMap: the map (kMapArrays n doubles) is staged in LDS (n <= kLdsMapMax: <= 62.4 KB, 600
 // waypoints at three lanes); larger maps are read from global memory (L2-resident) by the same code.
 constexpr int kLdsMapMax = 62400 / (8 * kMapArrays);
+
+// the velocity k_prep's car pass used for the car of iteration index it (src/main.cpp:1343-1346):
+// the table slot it (written or stale) with a car table, else row it plus its Monte-Carlo noise
+__device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_params& P, int64_t S,
+                                             int64_t s, int draw, bool tab, int it, double& vx, double& vy) {
+    const int64_t ix = (int64_t)it * S + s;
+    if (tab) { vx = in.tab_vx[ix]; vy = in.tab_vy[ix]; return; }
+    vx = in.car_vx[ix]; vy = in.car_vy[ix];
+    if (draw > 0) {
+        const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+        vx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, it, 2);
+        vy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, it, 3);
+    }
+}
 template <bool kLdsMap>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status) {
@@ -113,7 +132,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
         __syncthreads();
     }
-    const MapV m = map_view(kLdsMap ? smap : mg.buf, n);
+    const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
@@ -154,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     init_reference_waypoint(m, ego_x, ego_y, ref_wp, ratio);
     double ego_s = 0, ego_d = 0;
     int ego_lane = 0, nwp_unused = 0;
-    if (!lane_matching(m, ref_wp, ratio, ego_x, ego_y, ego_s, ego_d, ego_lane, nwp_unused)) {
+    if (!lane_match(m, ref_wp, ratio, ego_x, ego_y, ego_s, ego_d, ego_lane, nwp_unused)) {
         ego_s = ego_d = 0;
         ego_lane = 0;
         status |= PP_ST_EGO_UNMATCHED;
@@ -168,15 +187,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // LaneChangePlanner accumulation (src/main.cpp:377-445) and follow-car selection
     // (src/main.cpp:1388-1410) are order-dependent reductions over the same car sequence.
     const int T_in = in.prev_target_lane[s];
-    double lane_speed[NL], next_s[NL];
+    int lane_speed[NL];                     // the int-truncated lane speed where bit l of ls_set
+    int ls_set = 0;                         // (else P.max_speed)
+    double next_s[NL];
     bool open[NL];
-    int in_id = -1; double in_s = 0, in_vx = 0, in_vy = 0;
+    int in_id = -1; double in_s = 0;
     int t_id[NL];
-    double t_s[NL], t_vx[NL], t_vy[NL];
+    double t_s[NL];
 #pragma unroll
     for (int l = 0; l < NL; l++) {
-        lane_speed[l] = P.max_speed; next_s[l] = 1000; open[l] = true;
-        t_id[l] = -1; t_s[l] = 0; t_vx[l] = 0; t_vy[l] = 0;
+        lane_speed[l] = 0; next_s[l] = 1000; open[l] = true;
+        t_id[l] = -1; t_s[l] = 0;
     }
     int nmatched = 0;
     int ncar = in.n_cars[s];
@@ -191,8 +212,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
 #else
     const int iters = tab ? PP_MAX_CARS : ncar;
 #endif
+    // Visiting order. Every per-car reduction below is a minimum with ties to the lower iteration
+    // index (or an AND / a count), so any visiting order gives the reference's result once ties
+    // compare that index explicitly. Without a car table the rows are visited nearest first
+    // (squared distance to the ego, a 4-bit row index in the low mantissa bits of a float key,
+    // sorted by a Batcher network): the k-th visit of every lane of a wave then walks a similar
+    // number of lane segments in lane_matching, which is where the divergence was. With a table,
+    // or a negative car id (the reference's -1 'no car' sentinel), the identity order is kept.
+    uint64_t order = 0xFEDCBA9876543210ull;
+#if PP_CAR_SORT
+    if (!tab && iters > 1) {
+        uint32_t key[PP_MAX_CARS];
+        bool neg = false;
+#pragma unroll
+        for (int j = 0; j < PP_MAX_CARS; j++) {
+            key[j] = 0xFFFFFFF0u | (uint32_t)j;
+            if (j < iters) {
+                const int64_t ix = (int64_t)j * S + s;
+                const double dx = in.car_x[ix] - ego_x, dy = in.car_y[ix] - ego_y;
+                const float f = (float)(dx * dx + dy * dy);
+                key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
+                neg |= in.car_id[ix] < 0;
+            }
+        }
+#pragma unroll
+        for (int pw = 1; pw < PP_MAX_CARS; pw <<= 1)
+#pragma unroll
+            for (int k = pw; k >= 1; k >>= 1)
+#pragma unroll
+                for (int j = k % pw; j < PP_MAX_CARS - k; j += 2 * k)
+#pragma unroll
+                    for (int i = 0; i < k; i++)
+                        if ((i + j) / (2 * pw) == (i + j + k) / (2 * pw)) {
+                            const uint32_t lo = key[i + j] < key[i + j + k] ? key[i + j] : key[i + j + k];
+                            const uint32_t hi = key[i + j] < key[i + j + k] ? key[i + j + k] : key[i + j];
+                            key[i + j] = lo; key[i + j + k] = hi;
+                        }
+        if (!neg) {
+            order = 0;
+#pragma unroll
+            for (int j = 0; j < PP_MAX_CARS; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
+        }
+    }
+#endif
+    // iteration index of each running minimum, 4 bits each: next_s[l] at 4 l, the target-lane car
+    // of lane l at 4 (NL + l), the in-lane car at 8 NL (the follow cars' velocities are re-read
+    // from that index after the pass)
+    uint64_t its = 0;
+    auto it_of = [&](int f) { return (int)((its >> (4 * f)) & 15); };
+    auto set_it = [&](int f, int it) { its = (its & ~(15ull << (4 * f))) | ((uint64_t)it << (4 * f)); };
     int p = 0;                              // next unread row (table mode)
-    for (int it = 0; it < iters; it++) {
+    for (int kk = 0; kk < iters; kk++) {
+        const int it = (int)((order >> (4 * kk)) & 15);
         int row = it;
         if (tab) {
             while (p < ncar && in.car_id[(int64_t)p * S + s] < it) p++;     // ids must ascend
@@ -217,7 +288,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
 #ifdef PP_ABL_SKIP_FAR   // diagnostic timing build: cars beyond PP_ABL_SKIP_FAR metres skipped
             if ((cx - ego_x) * (cx - ego_x) + (cy - ego_y) * (cy - ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
 #endif
-            if (!lane_matching(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
+            PP_DIAGC(17, true);
+            if (!lane_match(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;
                 continue;
@@ -239,14 +311,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         // planner (src/main.cpp:379-444)
         const double sp = cs + cvs * dt0;
         if (sp > ego_s) {
-            if (sp < next_s[clane]) {
+            // the first car (in iteration order) with the smallest sp sets next_s; lane_speed
+            // comes from it if it is within 200 m (an earlier, larger minimum never is then)
+            // (next_s == 1000: still the initial value, which no car can set, so it wins the tie)
+            if (sp < next_s[clane] || (sp == next_s[clane] && next_s[clane] != 1000 && it < it_of(clane))) {
                 next_s[clane] = sp;
+                set_it(clane, it);
                 if (sp - ego_s < 200) {
                     int speed = (int)cvs;
                     if (speed > P.max_speed) speed = (int)P.max_speed;
                     if (sp - ego_s > 100)
                         speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
                     lane_speed[clane] = speed;
+                    ls_set |= 1 << clane;
+                } else {
+                    ls_set &= ~(1 << clane);
                 }
             }
         }
@@ -273,12 +352,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         const double s0 = cs + cvs * dt0;
         const double d0 = cd + cvd * dt0;
         if (s0 > ego_s && fabs(d0 - ego_d) < 3) {
-            if (in_id == -1 || in_s > s0) { in_id = id; in_s = s0; in_vx = cvx; in_vy = cvy; }
+            if (in_id == -1 || in_s > s0 || (in_s == s0 && it < it_of(2 * NL))) {
+                in_id = id; in_s = s0; set_it(2 * NL, it);
+            }
         }
 #pragma unroll
         for (int L = 0; L < NL; L++) {
             if (s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3) {
-                if (t_id[L] == -1 || t_s[L] > s0) { t_id[L] = id; t_s[L] = s0; t_vx[L] = cvx; t_vy[L] = cvy; }
+                if (t_id[L] == -1 || t_s[L] > s0 || (t_s[L] == s0 && it < it_of(NL + L))) {
+                    t_id[L] = id; t_s[L] = s0; set_it(NL + L, it);
+                }
             }
         }
     }
@@ -290,7 +373,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     for (int lane = 0; lane < NL; lane++) {
         score[lane] = 0;
         if (lane != ego_lane && !open[lane]) continue;
-        const double speed_score = s_min(lane_speed[lane] / P.max_speed, 1.0);
+        const double lsp = ((ls_set >> lane) & 1) ? (double)lane_speed[lane] : P.max_speed;
+        const double speed_score = s_min(lsp / P.max_speed, 1.0);
         const double distance_score = 1 - fabs((double)(T_in - lane)) / 2;
         const double free_score = s_min(1.0, next_s[lane] / 100);
         const double total = speed_score + distance_score / 2 + free_score;
@@ -319,6 +403,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     bool col;
     if (in_id >= 0) {
         double ts, tt;
+        double in_vx, in_vy;
+        car_velocity(in, P, S, s, draw, tab, it_of(2 * NL), in_vx, in_vy);
         const int code = limit_speed(P, in_vx, in_vy, in_s, ego_s, ego_speed, ego_acc, true, ts, tt, col);
         status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
         pv.in_ts[v] = ts; pv.in_tt[v] = tt;
@@ -328,7 +414,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     for (int L = 0; L < NL; L++) {
         if (t_id[L] >= 0 && t_id[L] != in_id) {
             double ts, tt;
-            const int code = limit_speed(P, t_vx[L], t_vy[L], t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
+            double t_vx, t_vy;
+            car_velocity(in, P, S, s, draw, tab, it_of(NL + L), t_vx, t_vy);
+            const int code = limit_speed(P, t_vx, t_vy, t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
             status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
             pv.l_ts[L * Sv + v] = ts; pv.l_tt[L * Sv + v] = tt;
             lim_mask |= 2 << L;
@@ -1491,6 +1579,9 @@ __global__ __launch_bounds__(256) void k_map_lengths(int n, double* g, double* t
         const double dx = lx - g[(4 + r) * n + p], dy = ly - g[(4 + NL + r) * n + p];
         const double len = sqrt(dx * dx + dy * dy);
         g[(4 + 2 * NL + r) * n + i] = len;                           // Map::get_lane_length
+        const double den = dx * dx + dy * dy;                         // helpers.h:202 rdenom
+        g[(4 + 3 * NL + r) * n + i] = den;
+        g[(4 + 4 * NL + r) * n + i] = 1.0 / den;
         t[0 * NL * n + r * n + i] = lx;
         t[1 * NL * n + r * n + i] = ly;
         t[2 * NL * n + r * n + i] = len;
@@ -1549,6 +1640,7 @@ struct pp_map {
     std::vector<double> geom;     // kMapArrays * n (MapG layout)
     std::vector<double> ptab;     // (4 + 2 NL) * n: ref xy, normal, lane centres (pp_map_geometry)
     std::vector<double> lanetab;  // 5 NL * n
+    int fastm = 0;                // MapV::fastm: every lane segment's rdenom in [2^-500, 2^500]
     DevState dev[kMaxDev];
     std::mutex mu;
 };
@@ -1571,6 +1663,9 @@ void fill_ptab(pp_map* M) {
         o[0] = g[i]; o[1] = g[n + i]; o[2] = g[2 * n + i]; o[3] = g[3 * n + i];
         for (int r = 0; r < NL; r++) { o[4 + 2 * r] = g[(4 + r) * n + i]; o[5 + 2 * r] = g[(4 + NL + r) * n + i]; }
     }
+    M->fastm = 1;
+    for (size_t i = (size_t)(4 + 3 * NL) * n; i < (size_t)(4 + 4 * NL) * n; i++)
+        if (!(g[i] >= 0x1p-500 && g[i] <= 0x1p500)) M->fastm = 0;
 }
 
 // Map::Init (src/main.cpp:89-131) + derived tables, on the host (done once per map).
@@ -1610,6 +1705,10 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
             const int p = W(i - 1);
             const double dx = lcx[r * n + i] - lcx[r * n + p], dy = lcy[r * n + i] - lcy[r * n + p];
             g[(4 + 2 * NL + r) * n + i] = std::sqrt(dx * dx + dy * dy);    // Map::get_lane_length
+            const double ex = lcx[r * n + p] - lcx[r * n + i], ey = lcy[r * n + p] - lcy[r * n + i];
+            const double den = ex * ex + ey * ey;                           // helpers.h:202 rdenom
+            g[(4 + 3 * NL + r) * n + i] = den;
+            g[(4 + 4 * NL + r) * n + i] = 1.0 / den;
         }
     }
     fill_ptab(M);
@@ -1769,9 +1868,9 @@ double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int3
 
 #ifdef PP_DIAG
 int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic builds only
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[32] = {};
+        unsigned long long z[64] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
@@ -1915,6 +2014,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
         mg.buf = M->dev[device].map;
         mg.n = M->n;
+        mg.fastm = M->fastm;
     }
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool timing = false;

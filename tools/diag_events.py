@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(REPO, "carnd-path-planning-project_amd"))
 
 NAMES = ["step", "seg_reload", "ramp_div", "wide_turn", "limiter", "override", "curv_adjust",
          "override_cls1", "wide_first_step", "dt_le_0", "limiter_ng0", "limiter_ng1", "limiter_ng2_4",
-         "limiter_ng5_9", "limiter_ng10_19", "limiter_ng20_"]
+         "limiter_ng5_9", "limiter_ng10_19", "limiter_ng20_", "match_walk_step", "car_match"]
 
 
 def main():
@@ -29,7 +29,7 @@ def main():
     prm = ppamd.default_params(n_speeds=5)
     scenes = ppamd.synth_device(m, S, seed=0x5EED0001, device=0)
     res = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
-    buf = (C.c_ulonglong * 32)()
+    buf = (C.c_ulonglong * 64)()
     lib.pp_diag_read(buf, 1)
     ppamd.evaluate(m, scenes, prm, res, device=0)
     torch.cuda.synchronize()
