@@ -464,12 +464,24 @@ __device__ __forceinline__ void sc_override(SC& c, double t, double speed) {
     const double mt = c.ttime * (speed - c.start) / (c.target - c.start);
     c.shift = t - mt;
 }
-// sc_override with r ~ 1 / (target - start) (ppm::div_rcp): the same quotient
+// sc_override with r ~ 1 / (target - start) (ppm::div_rcp): the same quotient. kChecked = false:
+// operands known in range (k_prep's speed/time check); a zero quotient's sign cannot matter here
+// (shift = t - mt).
+template <bool kChecked = true>
 __device__ __forceinline__ void sc_override_r(SC& c, double t, double speed, double r) {
     if (t > c.ttime) return;
     if (fabs(c.target - c.start) < kEps) return;
-    const double mt = ppm::div_rcp(c.ttime * (speed - c.start), c.target - c.start, r);
+    const double mt = kChecked ? ppm::div_rcp(c.ttime * (speed - c.start), c.target - c.start, r)
+                               : ppm::div_rcp_nc(c.ttime * (speed - c.start), c.target - c.start, r);
     c.shift = t - mt;
+}
+
+// k_cand<false>'s unchecked reciprocal divisions need every speed and ramp time of the scene's
+// candidates to be +0 or of magnitude in [2^-60, 2^20] (LimitSpeed targets may be negative): every
+// speed of a walk is then +0 or of magnitude in [2^-113, 2^21], every numerator of those
+// divisions inside [2^-400, 2^400]
+__device__ __forceinline__ bool speed_in_range(double x) {
+    return x == 0 ? !__builtin_signbit(x) : (fabs(x) >= 0x1p-60 && fabs(x) <= 0x1p20);
 }
 
 // LimitSpeed::calculate (src/main.cpp:1068-1150). Returns 0 FREEFLOW 1 BRAKE 2 MAXBRAKE 3 ADJUST 4 KEEP.

@@ -86,6 +86,10 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_CAR_SORT
 #define PP_CAR_SORT 1
 #endif
+// standing candidates (speed 0) take the turn series whatever the angle
+#ifndef PP_STAND_SERIES
+#define PP_STAND_SERIES 0
+#endif
 // phase A's serial steps (control-point distance rule, band sweeps) on the block's first wave
 #ifndef PP_SERIAL_WAVE
 #define PP_SERIAL_WAVE 1
@@ -436,6 +440,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
     // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
     if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
+    {   // k_cand<false> divides by reciprocals without range checks: speeds and ramp times in range
+        bool ok = speed_in_range(ego_speed);
+        for (int k = 0; k < P.n_speeds; k++) {
+            const double vk = cand_speed(P, ego_speed, k);
+            ok = ok && speed_in_range(vk) && speed_in_range(fabs(ego_speed - vk) / P.relaxed_acc);
+        }
+        if (lim_mask & 1) ok = ok && speed_in_range(pv.in_ts[v]) && speed_in_range(pv.in_tt[v]);
+#pragma unroll
+        for (int L = 0; L < NL; L++)
+            if (lim_mask & (2 << L)) ok = ok && speed_in_range(pv.l_ts[L * Sv + v]) && speed_in_range(pv.l_tt[L * Sv + v]);
+        if (!ok) lim_mask |= kLimSlow;
+    }
     pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
     double cm, sm, cp, sp_;
     ppm::sincos_pp<true>(-angle, sm, cm);
@@ -875,7 +891,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #define PP_SC_SPEED(t) sc_get_speed(sc, t)
 #endif
 #if PP_DIV_RCP & 2
-#define PP_DIV50(v) ppm::div_rcp(v, 50.0, 0.02)
+#define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div_rcp_nc(v, 50.0, 0.02))
 #else
 #define PP_DIV50(v) ((v) / 50)
 #endif
@@ -944,13 +960,16 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
         double adiff;
-        PP_DIAGC(3, !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
+        PP_DIAGC(3, !((dt > 0 && fabs(cr) <= ppm::kStepSinMax) || speed == 0));
         PP_DIAGC(8, ng == 0 && !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
         PP_DIAGC(9, !(dt > 0));
 #ifdef PP_ABL_NO_WIDE      // diagnostic timing build: every turn through the series
         if (true)
 #else
-        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1))
+        // a standing candidate (speed 0) turns by anything without consequence: its
+        // cacc = 0 * 50 * |adiff| is 0 for every finite adiff (and a curvature adjustment
+        // divides 0 by 0), so it takes the series whatever the angle (|cr| <= 1: finite)
+        if (__builtin_expect((dt > 0 && fabs(cr) <= ppm::kStepSinMax) || (PP_STAND_SERIES && speed == 0), 1))
 #endif
             adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
         else
@@ -985,7 +1004,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (na < 0) na = 0;
 #if PP_OVR_RCP
                 const double ns = prev_speed + PP_DIV50(na);
-                sc_override_r(sc, cur_t, ns, rds);
+                sc_override_r<kLarge>(sc, cur_t, ns, rds);
 #else
                 const double ns = prev_speed + na / 50;
                 sc_override(sc, cur_t, ns);
@@ -1138,17 +1157,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
     else { s0 = blockIdx.x / BPS; coff = (int)(blockIdx.x - s0 * BPS) * 256; }
     const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
     const int tid = threadIdx.x;
-    if (kSlow) {   // whole block leaves unless one of its scenes is flagged
-        const bool mine = tid < nsc && (pv.lim_mask[(s0 + tid) * D] & kLimSlow);
-        if (!__syncthreads_or(mine)) return;
+    // per scene: any of its draws flagged kLimSlow (absurd heading, or a speed or ramp time outside
+    // the range of the unchecked divisions) -> the scene runs in the k_cand<true> instantiation
+    uint32_t* sSlow = sFlags + SPB;
+    if (tid < SPB) { sFlags[tid] = 0; sSlow[tid] = 0; }
+    __syncthreads();
+    bool mine = false;
+    for (int t = tid; t < nsc * D; t += (int)blockDim.x) {
+        const int q = t / D;
+        if (pv.lim_mask[(s0 + q) * D + (t - q * D)] & kLimSlow) { atomicOr(&sSlow[q], 1u); mine = true; }
     }
-    if (tid < SPB) sFlags[tid] = 0;
+    if (!__syncthreads_or(mine) && kSlow) return;      // whole block leaves: no flagged scene
 #if PP_TEAM_SETUP
     {   // phase A: a team of TS threads per slot (team_a1..a5), block barriers between the steps
         int TS = (int)blockDim.x / nslot;
         if (TS > 8) TS = 8;
         const int j = tid / TS, r = tid - j * TS;
-        const bool act = j < NL * nsc && (((pv.lim_mask[(s0 + j / NL) * D] & kLimSlow) != 0) == kSlow);
+        const bool act = j < NL * nsc && ((sSlow[j / NL] != 0) == kSlow);
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         const int L = j % NL;
         const int64_t s = s0 + j / NL;
@@ -1160,7 +1185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         // slots fit the block's first wave, whose instruction stream is then the only one paying
         // for them (a team layout spreads them over every wave of the block)
         const int js = tid;
-        const bool act_s = js < NL * nsc && (((pv.lim_mask[(s0 + js / NL) * D] & kLimSlow) != 0) == kSlow);
+        const bool act_s = js < NL * nsc && ((sSlow[js / NL] != 0) == kSlow);
         const Slot sls = {sX + js * kKP, sY + js * kKP, sA + js * kKP, sB + js * kKP, sC + js * kKP, sMeta + 4 * js, 1};
         if (act_s) {
             const int64_t vs = (s0 + js / NL) * D;
@@ -1188,7 +1213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         if (!(PP_ABL_A & 4) && act) team_a5(sl, r, TS);
     }
 #else
-    if (tid < NL * nsc && (((pv.lim_mask[(s0 + tid / NL) * D] & kLimSlow) != 0) == kSlow)) {   // phase A
+    if (tid < NL * nsc && ((sSlow[tid / NL] != 0) == kSlow)) {   // phase A
         const int j = tid;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
         setup_lane(m, P, in, pv, s0 + j / NL, (s0 + j / NL) * D, Sv, j % NL, sl);
@@ -1220,7 +1245,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         sc_l = t / C;
         c = t - sc_l * C;
     }
-    if (sc_l < nsc && c < C && (((pv.lim_mask[(s0 + sc_l) * D] & kLimSlow) != 0) == kSlow)) {   // phase B
+    if (sc_l < nsc && c < C && ((sSlow[sc_l] != 0) == kSlow)) {   // phase B
         const int64_t s = s0 + sc_l;
         const int d = c / Cv, cc = c - d * Cv;
         const int64_t v = s * D + d;              // this draw's prep record
@@ -1288,7 +1313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
-    if (tid < nsc && (((pv.lim_mask[(s0 + tid) * D] & kLimSlow) != 0) == kSlow)) {
+    if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
         const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
         if (BPS == 1) out.status[s0 + tid] = st;
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
@@ -2061,7 +2086,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const int bps = C <= 256 ? 1 : (C + 255) / 256;
         const int threads = C <= 256 ? ((spb * C + 63) / 64) * 64 : 256;
         const int nslot = NL * spb;
-        const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * spb;
+        const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * spb;
         const int64_t blocks = bps == 1 ? (S + spb - 1) / spb : S * bps;
         if (blocks > 0x7fffffff) return PP_ERR_ARG;
         if (timing) (void)hipEventRecord(ev[1], st);

@@ -283,6 +283,14 @@ __device__ __forceinline__ double div_rcp(double n, double d, double r) {
     return an == 0.0 ? q0 : q;        // +-0 / d: q0 carries the quotient's sign
 }
 
+// div_rcp without its range checks, for operands known to stay in range: the caller's
+// k_cand<false> instantiation runs only scenes whose speeds and ramp times k_prep checked
+// (kLimSlow otherwise). The sign of a zero quotient may differ from the IEEE one.
+__device__ __forceinline__ double div_rcp_nc(double n, double d, double r) {
+    const double q0 = n * r;
+    return __builtin_fma(__builtin_fma(-q0, d, n), r, q0);
+}
+
 // n / d with r ~ 1/d for a d known to lie in [2^-450, 2^450] (dok: sqrt_rd's fast path);
 // otherwise, and for |n| outside [2^-900, 2^900], the IEEE division
 __device__ __forceinline__ double div_rcp_n(double n, double d, double r, bool dok) {
