@@ -954,6 +954,18 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const double ddx = x - pos_x, ddy = y - pos_y;
             ux = ddx * rd; uy = ddy * rd;
             if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
+#if PP_STEP_FAST
+            // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only in
+            // k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
+            // atan2(dy, dx) still has one; normalise the step scaled by its larger component
+            if (__builtin_expect(!dok, 0) && d == __builtin_inf() && fabs(ddx) <= 0x1.fffffffffffffp1023 &&
+                fabs(ddy) <= 0x1.fffffffffffffp1023) {
+                const double m = s_max(fabs(ddx), fabs(ddy));
+                const double a = ddx / m, b = ddy / m;
+                const double n = sqrt(a * a + b * b);
+                ux = a / n; uy = b / n;
+            }
+#endif
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
 #if PP_STEP_FAST

@@ -107,6 +107,27 @@ def compare(got, ref, check_cost=True):
     return e
 
 
+def compare_paths_free(env, scenes_dev, host, prm_kw, ref=None):
+    """The emit_paths=False evaluation (the bench's path) against the oracle. Without paths the
+    standstill quirk cannot be classified, so the all-paths evaluation of the same scenes is
+    compared with the oracle (compare) and the paths-free one with it: costs, winners, output
+    counts and status bit for bit (the same candidate arithmetic), next_x/next_y within TOL
+    (reference mode replays the winner's transform in k_emit)."""
+    got_e = run_gpu(env, scenes_dev, ppamd.default_params(emit_paths=True, **prm_kw))
+    if ref is None:
+        ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], host,
+                                     ppamd.default_params(emit_paths=True, **prm_kw), info=False)
+    e = compare(got_e, ref)
+    got = run_gpu(env, scenes_dev, ppamd.default_params(emit_paths=False, **prm_kw))
+    np.testing.assert_array_equal(got["cost"], got_e["cost"])
+    for k in ("winner", "n_out", "status"):
+        assert np.array_equal(got[k], got_e[k]), k
+    for k in ("next_x", "next_y"):
+        e = max(e, max_err(got[k], got_e[k]))
+    assert e <= TOL, e
+    return e
+
+
 def golden_params(**kw):
     return ppamd.default_params(n_speeds=int(G["n_speeds"]), speed_offsets=list(G["speed_offsets"]), **kw)
 
@@ -129,12 +150,19 @@ def test_golden_reference_vectors(env):
     print(f"golden: max |dxy| paths {e:.3e} m, next {e2:.3e} m")
 
 
-@pytest.mark.parametrize("mode", [ppamd.COST_REFERENCE, ppamd.COST_COMFORT])
-def test_random_scenes_vs_oracle(env, mode):
+@pytest.mark.parametrize("mode,emit", [(ppamd.COST_REFERENCE, True), (ppamd.COST_COMFORT, True),
+                                       (ppamd.COST_REFERENCE, False), (ppamd.COST_COMFORT, False)])
+def test_random_scenes_vs_oracle(env, mode, emit):
+    """emit=False is the bench's path: in reference mode k_cand records the winner's local path
+    and k_emit writes next_x/next_y; in comfort mode k_winner re-runs the argmin candidate."""
     S = 3000
     scenes = ppamd.synth_device(env["m"], S, seed=2024, first=10**6, device=0)
     host = ppamd.scenes_to_numpy(scenes)
-    prm = ppamd.default_params(cost_mode=mode, emit_paths=True)
+    if not emit:
+        e = compare_paths_free(env, scenes, host, {"cost_mode": mode})
+        print(f"random mode={mode} paths-free: max |dxy| {e:.3e} m")
+        return
+    prm = ppamd.default_params(cost_mode=mode, emit_paths=emit)
     got = run_gpu(env, scenes, prm)
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], host, prm, info=False)
     e = compare(got, ref)
@@ -158,6 +186,44 @@ def test_tied_cars_vs_oracle(env):
         assert np.array_equal(got["info"][k], ref["info"][k]), k
     np.testing.assert_allclose(got["info"]["lane_score"], ref["info"]["lane_score"], rtol=0, atol=1e-12)
     assert (got["info"]["in_lane_car"] >= 0).sum() > S // 4
+
+
+@pytest.mark.parametrize("emit", [True, False])
+def test_speed_range_edges_vs_oracle(env, emit):
+    """Speeds at the edges of k_cand<false>'s unchecked reciprocal divisions: telemetry speeds
+    of -0, subnormal, tiny, huge and negative magnitude (frame-0 scenes take the telemetry
+    speed), and a car just ahead in the ego lane whose velocity is 0, -0, subnormal or tiny (a
+    LimitSpeed target of that size). k_prep routes every scene with a speed or ramp time outside
+    the proven range to the checked instantiation; results must equal the oracle either way.
+    (Speeds of ~1e11 m/s and more put the path at ~1e10 m, where ulp-level differences of the
+    transcendentals exceed the absolute 1e-6 m tolerance: 3e6 mph = 1.3e6 m/s > 2^20 is the
+    largest finite magnitude used; 1e300 mph overflows to the same non-finite path on both sides.)"""
+    S = 1200
+    sc = ppamd.synth_host(env["m"], S, seed=909, first=31337)
+    speeds = [-0.0, 0.0, 5e-324, 1e-310, 1e-300, 1e-40, 1e-18, 2.237e-17, 1e-12, 1e-6, 0.3,
+              49.66, 3e6, 1e300, -3.0, -1e-300, 2.237 * 22.2]
+    vels = [0.0, -0.0, 5e-324, 1e-300, 1e-25, 1e-9, 3.0]
+    p9x, p9y = sc["prev_x"][9], sc["prev_y"][9]
+    hx, hy = p9x - sc["prev_x"][8], p9y - sc["prev_y"][8]
+    nrm = np.maximum(np.hypot(hx, hy), 1e-12)
+    for s in range(S):
+        if s % 3 != 2:
+            sc["n_prev"][s] = 0
+            sc["ego_speed_mph"][s] = speeds[s % len(speeds)]
+        if s % 2 == 0:
+            sc["car_x"][0, s] = p9x[s] + hx[s] / nrm[s] * 20.0
+            sc["car_y"][0, s] = p9y[s] + hy[s] / nrm[s] * 20.0
+            v = vels[(s // 2) % len(vels)]
+            sc["car_vx"][0, s] = v
+            sc["car_vy"][0, s] = v
+    if emit:
+        prm = ppamd.default_params(emit_paths=True)
+        got = run_gpu(env, to_dev(env, sc), prm)
+        ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+        e = compare(got, ref)
+    else:
+        e = compare_paths_free(env, to_dev(env, sc), sc, {})
+    print(f"speed edges (emit={emit}): max |dxy| {e:.3e} m")
 
 
 def test_device_synth_matches_host_synth(env):
