@@ -69,6 +69,12 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_STEP_FAST
 #define PP_STEP_FAST 1
 #endif
+#ifndef PP_WIDE_UNIT           // k_cand wide turns: atan2_unit + fmod_2pi_small (no fallbacks)
+#define PP_WIDE_UNIT 1
+#endif
+#ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
+#define PP_EMIT_CHUNK 4
+#endif
 #ifndef PP_EMIT_ROTATE
 #define PP_EMIT_ROTATE 1
 #endif
@@ -985,7 +991,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
             adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
         else
+#if PP_WIDE_UNIT
+            // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
+            adiff = ppm::fmod_2pi_small(ppm::atan2_unit(cr, dt) + 3 * kPi) - kPi;
+#else
             adiff = ppm::fmod_2pi(ppm::atan2_fast(cr, dt) + 3 * kPi) - kPi;
+#endif
 #else
         double adt;
         if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1)) adt = ppm::asin_small(cr);
@@ -1053,7 +1064,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     ppm::sincos_pp<kLarge>(tangle, sa, ca);
                 }
                 if (kOutMode == 3 && kRec) {
-                    double nad = nc / speed / 50;
+                    // rot only turns the output transform (k_emit), so it need not carry the
+                    // IEEE quotients' last bit: k_cand<false> divides by reciprocals (speed is +0
+                    // or in [2^-113, 2^21], nc in [0, maximum_acc]; speed 0 gives a NaN rot where
+                    // the IEEE quotient gives +-inf: both turn the rest of the path into NaN)
+                    double nad = kLarge ? nc / speed / 50
+                                        : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
                     rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
                     R.adj[ng >> 6] |= 1ull << (ng & 63);
@@ -1301,7 +1317,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
             }
+#ifdef PP_ABL_NO_REC       // diagnostic timing build: the first wave runs the cost-only loop too
+        } else if (false) {
+#else
         } else if (kMode == 1 && tid < 64) {
+#endif
             // reference mode, the block's first wave: the winners record their local path
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
             R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
@@ -1408,9 +1428,14 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
     const int room = N - K;
     const int ng = out.n_out[s] - K;
     const int64_t rstride = (int64_t)room * S;
-    for (int i = 0; i < K; i++) {
-        out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
-        out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+    {   // the kept previous points: every load issued before the first store
+        double kx[PP_PREV_KEEP], ky[PP_PREV_KEEP];
+#pragma unroll
+        for (int i = 0; i < PP_PREV_KEEP; i++)
+            if (i < K) { kx[i] = in.prev_x[(int64_t)i * S + s]; ky[i] = in.prev_y[(int64_t)i * S + s]; }
+#pragma unroll
+        for (int i = 0; i < PP_PREV_KEEP; i++)
+            if (i < K) { out.next_x[(int64_t)i * S + s] = kx[i]; out.next_y[(int64_t)i * S + s] = ky[i]; }
     }
     double cx = pv.pos_x[s], cy = pv.pos_y[s], tangle = pv.angle[s];
     double ca = pv.ca_p[s], sa = pv.sa_p[s];
@@ -1421,27 +1446,70 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
     // runs, with few lanes active, on most steps: it is kept short. The heading's sin/cos follow
     // by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead of sin/cos of the
     // accumulated angle (src/main.cpp:996-997): equal to ~1 ulp per adjustment.
-    for (int g = 0; g < ng; g++) {
-        const bool bit = (g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0;
-        if (bit) {
-            const double rot = rec[2 * rstride + (int64_t)g * S + s];
-            double cr, sr;
-            ppm::sincos_pp<true>(rot, sr, cr);
-            const double tpx = (pxp * ca - pyp * sa) + cx;
-            const double tpy = (pxp * sa + pyp * ca) + cy;
-            const double vx = cx - tpx, vy = cy - tpy;
-            cx = tpx + (vx * cr - vy * sr);
-            cy = tpy + (vx * sr + vy * cr);
-            const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
-            ca = nca; sa = nsa;
+    // Steps are taken kEmitChunk at a time with all of the chunk's record loads (the rotation
+    // only where the step's bit is set) in flight together: one memory round trip per chunk
+    // instead of one or two per step.
+    // A rotation beyond sincos_pp's medium range (a step that slowed to ~1e-7 m/s) sends the
+    // lane's chunk through a per-step loop with the library reduction, re-reading the record:
+    // the unrolled chunk then holds no call and stays register-light.
+    constexpr int kEmitChunk = PP_EMIT_CHUNK;
+    auto rotate = [&](double rot, double& cr, double& sr) {
+        const double tpx = (pxp * ca - pyp * sa) + cx;
+        const double tpy = (pxp * sa + pyp * ca) + cy;
+        const double vx = cx - tpx, vy = cy - tpy;
+        cx = tpx + (vx * cr - vy * sr);
+        cy = tpy + (vx * sr + vy * cr);
+        const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
+        ca = nca; sa = nsa;
+        (void)rot;
+    };
+    for (int g0 = 0; g0 < ng; g0 += kEmitChunk) {
+        double px_[kEmitChunk], py_[kEmitChunk], rt[kEmitChunk];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int u = 0; u < kEmitChunk; u++) {
+            const int g = g0 + u;
+            const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
+            bits |= bit ? 1u << u : 0u;
+            px_[u] = g < ng ? rec[(int64_t)g * S + s] : 0.0;
+            py_[u] = g < ng ? rec[rstride + (int64_t)g * S + s] : 0.0;
+            rt[u] = bit ? rec[2 * rstride + (int64_t)g * S + s] : 0.0;
         }
-        const double px_ = rec[(int64_t)g * S + s], py_ = rec[rstride + (int64_t)g * S + s];
-        const double tx = px_ * ca - py_ * sa;
-        const double ty = px_ * sa + py_ * ca;
-        out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
-        out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
-        pxp = px_;
-        pyp = py_;
+        bool huge = false;
+#pragma unroll
+        for (int u = 0; u < kEmitChunk; u++) huge |= !(fabs(rt[u]) <= ppm::kMediumMax);
+        if (__builtin_expect(huge, 0)) {
+            for (int g = g0; g < ng && g < g0 + kEmitChunk; g++) {
+                if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
+                    const double rot = rec[2 * rstride + (int64_t)g * S + s];
+                    double cr, sr;
+                    ppm::sincos_pp<true>(rot, sr, cr);
+                    rotate(rot, cr, sr);
+                }
+                const double qx = rec[(int64_t)g * S + s], qy = rec[rstride + (int64_t)g * S + s];
+                out.next_x[(int64_t)(K + g) * S + s] = (qx * ca - qy * sa) + cx;
+                out.next_y[(int64_t)(K + g) * S + s] = (qx * sa + qy * ca) + cy;
+                pxp = qx;
+                pyp = qy;
+            }
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < kEmitChunk; u++) {
+            const int g = g0 + u;
+            if (g >= ng) break;
+            if ((bits >> u) & 1) {
+                double cr, sr;
+                ppm::sincos_pp<false>(rt[u], sr, cr);
+                rotate(rt[u], cr, sr);
+            }
+            const double tx = px_[u] * ca - py_[u] * sa;
+            const double ty = px_[u] * sa + py_[u] * ca;
+            out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
+            out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+            pxp = px_[u];
+            pyp = py_[u];
+        }
     }
     (void)tangle;
 #else

@@ -239,6 +239,44 @@ __device__ __forceinline__ double atan2_fast(double y, double x) {
     return m == 0 ? zz : m == 1 ? -zz : m == 2 ? pi - (zz - pi_lo) : (zz - pi_lo) - pi;
 }
 
+// atan2_fast for finite (y, x) that are not both zero (the wide-turn branch of the candidate
+// loop: components of unit vectors): no special-case fallback. Zero, tiny (|y/x| < 2^-60) and huge
+// (> 2^60) ratios go through the same reduction: t = 0 or a tiny/huge-ratio t gives the values
+// atan2_pp returns for them (+-0, +-pi/2, +-pi: hi + lo and pi - (t - pi_lo) round to those
+// constants), NaN propagates. tools/atan2_check.hip compares the two on the GPU.
+__device__ __forceinline__ double atan2_unit(double y, double x) {
+    const double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    const int hy = hiword(y);
+    const double ay = fabs(y), ax = fabs(x);
+    const double y16 = 16.0 * ay;
+    const int id = (y16 < 7.0 * ax) ? -1 : (y16 < 11.0 * ax) ? 0 : (y16 < 19.0 * ax) ? 1
+                 : (y16 < 39.0 * ax) ? 2 : 3;
+    double num, den, hi, lo;
+    if (id < 0)       { num = ay;                  den = ax;                  hi = 0.0; lo = 0.0; }
+    else if (id == 0) { num = 2.0 * ay - ax;       den = 2.0 * ax + ay;
+                        hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+    else if (id == 1) { num = ay - ax;             den = ax + ay;
+                        hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+    else if (id == 2) { num = 2.0 * ay - 3.0 * ax; den = 2.0 * ax + 3.0 * ay;
+                        hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+    else              { num = -ax;                 den = ay;
+                        hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    const double t = num / den;
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const double z = t * t;
+    const double w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const double zz = (id < 0) ? t - t * (s1 + s2) : hi - ((t * (s1 + s2) - lo) - t);
+    const int m = ((hy >> 31) & 1) | (x < 0.0 ? 2 : 0);   // x = -0 counts as +0 (atan2(y, -0) = +-pi/2)
+    return m == 0 ? zz : m == 1 ? -zz : m == 2 ? pi - (zz - pi_lo) : (zz - pi_lo) - pi;
+}
+
 // Angle between consecutive step directions without atan2 (run_candidate). The reference turns
 // each step (dx, dy) into an absolute angle atan2(dy, dx) and wraps the difference to the previous
 // one (src/main.cpp:934). For unit vectors u_prev, u the signed angle is asin(u_prev x u) while
@@ -332,6 +370,13 @@ __device__ __forceinline__ bool sqrt_rd(double q, double& d, double& rd) {
 // (Sterbenz: y <= a < 4y for the k = 2 case, with 2y and 3y exact doubles). Other finite inputs
 // are reduced by exact subtractions of y * 2^j (each r - y*2^j with y*2^j <= r < y*2^(j+1) is
 // exact by Sterbenz), the textbook long division fmod performs.
+// fmod_2pi for a in [0, 3 * 2pi) or NaN (a = atan2 + 3 pi): its first three cases; NaN - 2y = NaN
+__device__ __forceinline__ double fmod_2pi_small(double a) {
+    const double y = 2 * 3.14159265358979323846;
+    if (a < y) return a;
+    if (a < 2.0 * y) return a - y;
+    return a - 2.0 * y;
+}
 __device__ __forceinline__ double fmod_2pi(double a) {
     const double y = 2 * 3.14159265358979323846;
     if (a >= 0.0 && a < y) return a;
