@@ -445,11 +445,14 @@ __device__ __forceinline__ double sc_get_speed(const SC& c, double t) {
     return c.start + (c.target - c.start) * t / c.ttime;
 }
 // sc_get_speed with r ~ 1/ttime (ppm::div_rcp): the same quotient
+// kChecked = false: ramp times known in range (k_prep's check; k_cand<false>), no range checks
+template <bool kChecked = true>
 __device__ __forceinline__ double sc_get_speed_r(const SC& c, double t, double r) {
     t -= c.shift;
     if (t < 0) t = 0;
     if (t > c.ttime) return c.target;
-    return c.start + ppm::div_rcp((c.target - c.start) * t, c.ttime, r);
+    return c.start + (kChecked ? ppm::div_rcp((c.target - c.start) * t, c.ttime, r)
+                               : ppm::div_rcp_nc((c.target - c.start) * t, c.ttime, r));
 }
 __device__ __forceinline__ void sc_add_limit(SC& c, double nts, double ntt) {
     const double tm = s_max(c.ttime, 0.02);

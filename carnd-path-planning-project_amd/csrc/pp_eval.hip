@@ -72,6 +72,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_WIDE_UNIT           // k_cand wide turns: atan2_unit + fmod_2pi_small (no fallbacks)
 #define PP_WIDE_UNIT 1
 #endif
+#ifndef PP_LOOP_UNROLL         // candidate loop unroll factor (loop-carried step direction copies)
+#define PP_LOOP_UNROLL 1
+#endif
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
@@ -105,9 +108,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #endif
 // Divisions of the candidate loop as a reciprocal and one correction step (ppm::div_rcp):
 // bit 0: the two divisions by the step length d, bit 1: speed / 50, bit 2: the speed ramp / ttime
-// (bit 2 is off: keeping 1/ttime current through the overrides costs more than it saves)
+// (bit 2: k_cand<false> divides the ramp unchecked; k_cand<true> keeps the checked form)
 #ifndef PP_DIV_RCP
-#define PP_DIV_RCP 3
+#define PP_DIV_RCP 7
 #endif
 // the override's divisions (na / 50 and SpeedController::override_speed) by reciprocals
 #ifndef PP_OVR_RCP
@@ -892,14 +895,17 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
 #if PP_DIV_RCP & 4
     double rtt = ppm::rcp_nr(sc.ttime);
-#define PP_SC_SPEED(t) sc_get_speed_r(sc, t, rtt)
+#define PP_SC_SPEED(t) sc_get_speed_r<kLarge>(sc, t, rtt)
 #else
 #define PP_SC_SPEED(t) sc_get_speed(sc, t)
 #endif
 #if PP_DIV_RCP & 2
-#define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div_rcp_nc(v, 50.0, 0.02))
+#define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div50_nc(v))
 #else
 #define PP_DIV50(v) ((v) / 50)
+#endif
+#if PP_LOOP_UNROLL > 1
+#pragma unroll PP_LOOP_UNROLL
 #endif
     while (arg < 50 && ng < room) {
         PP_DIAGC(0, true);

@@ -13,6 +13,22 @@
 
 namespace ppm {
 
+// a * b + c as the three-address v_fma_f64. The compiler lowers __builtin_fma with a register
+// addend that stays live (a loop-invariant polynomial coefficient) to v_mov_b64 + the two-address
+// v_fmac_f64, one extra issue per term; PP_FMA3=0 keeps __builtin_fma.
+#ifndef PP_FMA3
+#define PP_FMA3 1
+#endif
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+#if PP_FMA3
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return __builtin_fma(a, b, c);
+#endif
+}
+
 __device__ __forceinline__ int hiword(double x) { return (int)(__double_as_longlong(x) >> 32); }
 __device__ __forceinline__ unsigned loword(double x) { return (unsigned)__double_as_longlong(x); }
 __device__ __forceinline__ double from_words(int hi, unsigned lo) {
@@ -244,6 +260,13 @@ __device__ __forceinline__ double atan2_fast(double y, double x) {
 // (> 2^60) ratios go through the same reduction: t = 0 or a tiny/huge-ratio t gives the values
 // atan2_pp returns for them (+-0, +-pi/2, +-pi: hi + lo and pi - (t - pi_lo) round to those
 // constants), NaN propagates. tools/atan2_check.hip compares the two on the GPU.
+// atan_pos's interval constants (hi, lo) for id = -1 .. 3 (atan2_unit)
+__constant__ double kAtanHiLo[10] = {
+    0.0, 0.0,
+    4.63647609000806093515e-01, 2.26987774529616870924e-17,
+    7.85398163397448278999e-01, 3.06161699786838301793e-17,
+    9.82793723247329054082e-01, 1.39033110312309984516e-17,
+    1.57079632679489655800e+00, 6.12323399573676603587e-17};
 __device__ __forceinline__ double atan2_unit(double y, double x) {
     const double pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
     const int hy = hiword(y);
@@ -251,16 +274,15 @@ __device__ __forceinline__ double atan2_unit(double y, double x) {
     const double y16 = 16.0 * ay;
     const int id = (y16 < 7.0 * ax) ? -1 : (y16 < 11.0 * ax) ? 0 : (y16 < 19.0 * ax) ? 1
                  : (y16 < 39.0 * ax) ? 2 : 3;
-    double num, den, hi, lo;
-    if (id < 0)       { num = ay;                  den = ax;                  hi = 0.0; lo = 0.0; }
-    else if (id == 0) { num = 2.0 * ay - ax;       den = 2.0 * ax + ay;
-                        hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
-    else if (id == 1) { num = ay - ax;             den = ax + ay;
-                        hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
-    else if (id == 2) { num = 2.0 * ay - 3.0 * ax; den = 2.0 * ax + 3.0 * ay;
-                        hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
-    else              { num = -ax;                 den = ay;
-                        hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    double num, den;
+    if (id < 0)       { num = ay;                  den = ax; }
+    else if (id == 0) { num = 2.0 * ay - ax;       den = 2.0 * ax + ay; }
+    else if (id == 1) { num = ay - ax;             den = ax + ay; }
+    else if (id == 2) { num = 2.0 * ay - 3.0 * ax; den = 2.0 * ax + 3.0 * ay; }
+    else              { num = -ax;                 den = ay; }
+    // the interval constants by a per-lane table load: the branch is rare, and constants
+    // selected in registers would be hoisted out of the candidate loop and held there
+    const double hi = kAtanHiLo[2 * (id + 1)], lo = kAtanHiLo[2 * (id + 1) + 1];
     const double t = num / den;
     const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
                  aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
@@ -291,11 +313,11 @@ __device__ __forceinline__ double asin_small(double s) {
                  c3 = 4.46428571428571428571e-02, c4 = 3.03819444444444444444e-02,
                  c5 = 2.23721590909090909091e-02, c6 = 1.73527644230769230769e-02;
     const double z = s * s;
-    double p = __builtin_fma(z, c6, c5);
-    p = __builtin_fma(z, p, c4);
-    p = __builtin_fma(z, p, c3);
-    p = __builtin_fma(z, p, c2);
-    p = __builtin_fma(z, p, c1);
+    double p = fma3(z, c6, c5);
+    p = fma3(z, p, c4);
+    p = fma3(z, p, c3);
+    p = fma3(z, p, c2);
+    p = fma3(z, p, c1);
     return __builtin_fma(s * z, p, s);
 }
 // 1/d to ~1 ulp: v_rcp_f64 and two Newton steps (d finite, normal)
@@ -327,6 +349,19 @@ __device__ __forceinline__ double div_rcp(double n, double d, double r) {
 __device__ __forceinline__ double div_rcp_nc(double n, double d, double r) {
     const double q0 = n * r;
     return __builtin_fma(__builtin_fma(-q0, d, n), r, q0);
+}
+
+// div_rcp_nc(v, 50, 0.02) with the residual fma written three-address (v stays live after it, so
+// the compiler's two-address v_fmac would need a copy of v first); 50 from an SGPR pair
+__device__ __forceinline__ double div50_nc(double v) {
+    const double q0 = v * 0.02;
+#if PP_FMA3
+    double e;
+    asm("v_fma_f64 %0, -%1, %2, %3" : "=v"(e) : "v"(q0), "s"(50.0), "v"(v));
+    return __builtin_fma(e, 0.02, q0);
+#else
+    return __builtin_fma(__builtin_fma(-q0, 50.0, v), 0.02, q0);
+#endif
 }
 
 // n / d with r ~ 1/d for a d known to lie in [2^-450, 2^450] (dok: sqrt_rd's fast path);
