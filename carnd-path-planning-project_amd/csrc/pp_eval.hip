@@ -75,6 +75,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_LOOP_UNROLL         // candidate loop unroll factor (loop-carried step direction copies)
 #define PP_LOOP_UNROLL 1
 #endif
+#ifndef PP_SPL_A0              // cached spline segment: extrapolation folded into the cubic form
+#define PP_SPL_A0 1
+#endif
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
@@ -940,11 +943,18 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
             seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
             seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
-            sx = sl.x(idx); sa_ = sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+            sx = sl.x(idx); sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
         }
 #endif
         const double h = x - sx;
         double y;
+#if PP_SPL_A0
+        // kCache segments: the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0
+        // (0 h + b = b, and at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the
+        // last knot, whose a is 0 (spline.h:367): one polynomial form for every step
+        if (kCache && PP_SEG_MODE != 2) y = ((sa_ * h + sb) * h + sc_) * h + sy;
+        else
+#endif
         if (cnt == 0 && x < sx) y = (sb * h + sc_) * h + sy;                       // left
         else if (cnt == nk && x > sx) y = (sb * h + sc_) * h + sy;                 // right
         else y = ((sa_ * h + sb) * h + sc_) * h + sy;
