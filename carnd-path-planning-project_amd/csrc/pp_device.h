@@ -449,7 +449,8 @@ __device__ __forceinline__ double sc_get_speed(const SC& c, double t) {
 template <bool kChecked = true>
 __device__ __forceinline__ double sc_get_speed_r(const SC& c, double t, double r) {
     t -= c.shift;
-    if (t < 0) t = 0;
+    // unchecked: t - shift is never NaN (finite in-range operands), so max(t, 0) is v_max_f64
+    if (kChecked) { if (t < 0) t = 0; } else t = __builtin_fmax(t, 0.0);
     if (t > c.ttime) return c.target;
     return c.start + (kChecked ? ppm::div_rcp((c.target - c.start) * t, c.ttime, r)
                                : ppm::div_rcp_nc((c.target - c.start) * t, c.ttime, r));

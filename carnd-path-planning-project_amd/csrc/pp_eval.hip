@@ -975,18 +975,22 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         {
             const double ddx = x - pos_x, ddy = y - pos_y;
             ux = ddx * rd; uy = ddy * rd;
-            if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
 #if PP_STEP_FAST
-            // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only in
-            // k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
-            // atan2(dy, dx) still has one; normalise the step scaled by its larger component
-            if (__builtin_expect(!dok, 0) && d == __builtin_inf() && fabs(ddx) <= 0x1.fffffffffffffp1023 &&
-                fabs(ddy) <= 0x1.fffffffffffffp1023) {
-                const double m = s_max(fabs(ddx), fabs(ddy));
-                const double a = ddx / m, b = ddy / m;
-                const double n = sqrt(a * a + b * b);
-                ux = a / n; uy = b / n;
+            if (__builtin_expect(!dok, 0)) {        // d == 0 implies !dok (q = 0 < 2^-900)
+                if (d == 0) { ux = 1.0; uy = 0.0; }
+                // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only
+                // in k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
+                // atan2(dy, dx) still has one; normalise the step scaled by its larger component
+                if (d == __builtin_inf() && fabs(ddx) <= 0x1.fffffffffffffp1023 &&
+                    fabs(ddy) <= 0x1.fffffffffffffp1023) {
+                    const double m = s_max(fabs(ddx), fabs(ddy));
+                    const double a = ddx / m, b = ddy / m;
+                    const double n = sqrt(a * a + b * b);
+                    ux = a / n; uy = b / n;
+                }
             }
+#else
+            if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
 #endif
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
@@ -1102,8 +1106,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         prev_angle = astep;
 #endif
 #if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS && PP_STEP_FAST
-        const double sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
-        pos_y += ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok);
+        const double sp_step = kLarge ? ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok)
+                                      : ppm::div_rcp_d((x - pos_x) * dstep, d, rd, dok);
+        pos_y += kLarge ? ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok)
+                        : ppm::div_rcp_d((y - pos_y) * dstep, d, rd, dok);
 #elif (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
         const double sp_step = ppm::div_rcp((x - pos_x) * dstep, d, rd);
         pos_y += ppm::div_rcp((y - pos_y) * dstep, d, rd);

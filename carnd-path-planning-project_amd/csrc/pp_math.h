@@ -375,6 +375,17 @@ __device__ __forceinline__ double div_rcp_n(double n, double d, double r, bool d
     return q;
 }
 
+// div_rcp_n for k_cand<false>: the numerators (x - pos_x) dstep and (y - pos_y) dstep with dstep
+// +0 or in [2^-119, 2^15] stay below 2^900, and a numerator below 2^-900 (a step of ~1e-150 m and
+// less) may take an ulp of error only at that scale; so only d's range (dok) picks the IEEE
+// division. n = +-0 gives q0 = +-0 and a zero correction, as the IEEE quotient.
+__device__ __forceinline__ double div_rcp_d(double n, double d, double r, bool dok) {
+    const double q0 = n * r;
+    const double q = __builtin_fma(__builtin_fma(-q0, d, n), r, q0);
+    if (__builtin_expect(!dok, 0)) return n / d;
+    return q;
+}
+
 // d = sqrt(q) correctly rounded and rd ~ 1/d; returns whether q was in [2^-900, 2^900]. There
 // this is the ISA sequence the compiler emits for an IEEE sqrt (v_rsq_f64, then Goldschmidt
 // g ~ sqrt(q), h ~ 1/(2 sqrt(q)) and two residual corrections of g), without its range scaling
