@@ -473,6 +473,12 @@ __device__ __forceinline__ void sc_override(SC& c, double t, double speed) {
 // (shift = t - mt).
 template <bool kChecked = true>
 __device__ __forceinline__ void sc_override_r(SC& c, double t, double speed, double r) {
+    if (!kChecked) {      // the two early returns as a select (r = 1/(target - start) may be inf)
+        const double mt = ppm::div_rcp_nc(c.ttime * (speed - c.start), c.target - c.start, r);
+        const bool keep = t > c.ttime || fabs(c.target - c.start) < kEps;
+        c.shift = keep ? c.shift : t - mt;
+        return;
+    }
     if (t > c.ttime) return;
     if (fabs(c.target - c.start) < kEps) return;
     const double mt = kChecked ? ppm::div_rcp(c.ttime * (speed - c.start), c.target - c.start, r)
