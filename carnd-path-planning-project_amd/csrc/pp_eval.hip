@@ -1106,10 +1106,18 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         prev_angle = astep;
 #endif
 #if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS && PP_STEP_FAST
-        const double sp_step = kLarge ? ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok)
-                                      : ppm::div_rcp_d((x - pos_x) * dstep, d, rd, dok);
-        pos_y += kLarge ? ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok)
-                        : ppm::div_rcp_d((y - pos_y) * dstep, d, rd, dok);
+        double sp_step, dpy;
+        if (kLarge) {
+            sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
+            dpy = ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok);
+        } else {          // ppm::div_rcp_d for both numerators, one !dok branch
+            const double nx = (x - pos_x) * dstep, ny = (y - pos_y) * dstep;
+            const double qx = nx * rd, qy = ny * rd;
+            sp_step = __builtin_fma(__builtin_fma(-qx, d, nx), rd, qx);
+            dpy = __builtin_fma(__builtin_fma(-qy, d, ny), rd, qy);
+            if (__builtin_expect(!dok, 0)) { sp_step = nx / d; dpy = ny / d; }
+        }
+        pos_y += dpy;
 #elif (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
         const double sp_step = ppm::div_rcp((x - pos_x) * dstep, d, rd);
         pos_y += ppm::div_rcp((y - pos_y) * dstep, d, rd);
