@@ -305,7 +305,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             if ((cx - ego_x) * (cx - ego_x) + (cy - ego_y) * (cy - ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
 #endif
             PP_DIAGC(17, true);
+#ifdef PP_ABL_NO_MATCH     // diagnostic timing build: no lane matching of the cars
+            cs = ego_s + (cx - ego_x); cd = 6.0 + 0.1 * (cy - ego_y); clane = 1; nwp = ref_wp;
+            if (false) {
+#else
             if (!lane_match(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
+#endif
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;
                 continue;
