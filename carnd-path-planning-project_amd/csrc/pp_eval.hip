@@ -40,6 +40,7 @@ __device__ __forceinline__ void diag(int k, bool c) {
 #define PP_DIAGC(k, c) ((void)0)
 #endif
 #include "pp_device.h"
+#include "pp_glibcm.h"
 #include "pp_math.h"
 #include "pp_synth.h"
 
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
         const double vx = pos_x - p8x, vy = pos_y - p8y;
         if (vx * vx + vy * vy < kEps) angle = yaw * kPi / 180;
-        else angle = ppm::atan2_pp(pos_y - p8y, pos_x - p8x);
+        else angle = ppg::atan2(pos_y - p8y, pos_x - p8x);      // glibc's atan2, bit for bit
     }
     // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
     // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
@@ -470,9 +471,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         if (!ok) lim_mask |= kLimSlow;
     }
     pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
+    // the frame's rotations cos(-angle), sin(-angle) (:786-787) and cos(angle), sin(angle)
+    // (:822-823) as the reference's libm computes them (pp_glibcm.h): every knot is a product with
+    // them, so the spline and every path position carry their exact bits. Headings of 1e8 rad and
+    // more (only from an absurd telemetry yaw) are outside the restated reduction.
     double cm, sm, cp, sp_;
-    ppm::sincos_pp<true>(-angle, sm, cm);
-    ppm::sincos_pp<true>(angle, sp_, cp);
+    if (!(ppg::cos(-angle, cm) && ppg::sin(-angle, sm) && ppg::cos(angle, cp) && ppg::sin(angle, sp_))) {
+        ppm::sincos_pp<true>(-angle, sm, cm);
+        ppm::sincos_pp<true>(angle, sp_, cp);
+    }
     pv.ca_m[v] = cm; pv.sa_m[v] = sm;
     pv.ca_p[v] = cp; pv.sa_p[v] = sp_;
     pv.ego_speed[v] = ego_speed; pv.ego_d[v] = ego_d; pv.ego_vd[v] = ego_vd;
@@ -1629,7 +1636,7 @@ __global__ __launch_bounds__(256) void k_sim(ppsynth::LaneTables LT, pp_scene_ba
     const double dist = sqrt(dx * dx + dy * dy);
     ex[s] = nx; ey[s] = ny;
     espd[s] = dist * 50 * 2.237;
-    if (dist > 0) eyaw[s] = atan2(dy, dx) * 180.0 / kPi;
+    if (dist > 0) eyaw[s] = ppg::atan2(dy, dx) * 180.0 / kPi;
     const int np = n_out - kk;
     for (int i = 0; i < PP_PREV_KEEP; i++) {
         const bool ok = i < np;
@@ -1697,10 +1704,12 @@ __global__ __launch_bounds__(256) void k_map_lanes(int n, double* g) {
     const int q = wrap_i(i + 1, n);
     const double nx = g[2 * n + i], ny = g[3 * n + i];
     double ax = (nx + g[2 * n + q]) / 2, ay = (ny + g[3 * n + q]) / 2;
-    const double a_n = ppm::atan2_pp(ny, nx);
-    const double a_avg = ppm::atan2_pp(ay, ax);
-    double s_, c_;
-    ppm::sincos_pp<true>(a_avg - a_n, s_, c_);
+    // the host's std::atan2 / std::cos (glibc) restated bit for bit (pp_glibcm.h): the device map
+    // equals pp_map_create's (|a_avg - a_n| < pi, inside the restated cos domain)
+    const double a_n = ppg::atan2(ny, nx);
+    const double a_avg = ppg::atan2(ay, ax);
+    double c_;
+    if (!ppg::cos(a_avg - a_n, c_)) c_ = __builtin_nan("");
     ax /= c_;
     ay /= c_;
     for (int r = 0; r < NL; r++) {
@@ -1728,6 +1737,17 @@ __global__ __launch_bounds__(256) void k_map_lengths(int n, double* g, double* t
         t[3 * NL * n + r * n + i] = dx / len;
         t[4 * NL * n + r * n + i] = dy / len;
     }
+}
+
+// the restated libm on the device (pp_libm_eval; parity tests of pp_glibcm.h's device build)
+__global__ __launch_bounds__(256) void k_libm(int kind, const double* a, const double* b, double* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double r = __builtin_nan("");
+    if (kind == 0) ppg::sin(a[i], r);
+    else if (kind == 1) ppg::cos(a[i], r);
+    else r = ppg::atan2(a[i], b[i]);
+    out[i] = r;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2016,6 +2036,29 @@ int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic b
     return 0;
 }
 #endif
+int32_t pp_libm_eval(int32_t kind, const double* a, const double* b, double* out, int64_t n,
+                     int32_t device, void* hip_stream) {
+    if (kind < 0 || kind > 2 || n < 0 || (n > 0 && (!a || !out || (kind == 2 && !b))) || device < -1 ||
+        device >= kMaxDev)
+        return PP_ERR_ARG;
+    if (n == 0) return PP_OK;
+    if (device < 0) {
+        for (int64_t i = 0; i < n; i++) {
+            double r = __builtin_nan("");
+            if (kind == 0) ppg::sin(a[i], r);
+            else if (kind == 1) ppg::cos(a[i], r);
+            else r = ppg::atan2(a[i], b[i]);
+            out[i] = r;
+        }
+        return PP_OK;
+    }
+    DeviceGuard g(device);
+    const int64_t blocks = (n + 255) / 256;
+    if (blocks > 0x7fffffff) return PP_ERR_ARG;
+    hipLaunchKernelGGL(k_libm, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)hip_stream, kind, a, b, out, n);
+    return hipGetLastError() == hipSuccess ? PP_OK : PP_ERR_HIP;
+}
+
 const char* pp_version(void) { return "pp-mi355x 0.1 (gfx950, fp64, lane-per-candidate)"; }
 
 int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** out) {

@@ -17,6 +17,8 @@
 #include <stdint.h>
 #include <math.h>
 
+#include "pp_glibcm.h"
+
 #ifndef PP_HD
 #define PP_HD __host__ __device__
 #endif
@@ -222,7 +224,7 @@ PP_HD inline void synth_scene(const LaneTables& T, uint64_t seed, int64_t g, int
     }
     o.ego_x[local] = ex;
     o.ego_y[local] = ey;
-    o.ego_yaw_deg[local] = atan2(euy, eux) * 180.0 / 3.14159265358979323846;
+    o.ego_yaw_deg[local] = ppg::atan2(euy, eux) * 180.0 / 3.14159265358979323846;   // glibc's, host == device
     o.ego_speed_mph[local] = v * 2.237;
     o.n_prev[local] = frame0 ? 0 : 10;
     o.prev_target_lane[local] = ptl;

@@ -134,7 +134,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
            "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device",
-           "pp_num_lanes"]
+           "pp_num_lanes", "pp_libm_eval"]
 
 
 def _load():
@@ -205,6 +205,8 @@ def _load():
     lib.pp_control_format_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                              C.c_int64, C.c_void_p, C.c_int32, C.c_void_p]
     lib.pp_control_format_device.restype = C.c_int32
+    lib.pp_libm_eval.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
+    lib.pp_libm_eval.restype = C.c_int32
     return lib
 
 
@@ -544,6 +546,27 @@ def highway_map():
 
 def version() -> str:
     return lib.pp_version().decode()
+
+
+LIBM_KINDS = {"sin": 0, "cos": 1, "atan2": 2}
+
+
+def libm_eval(kind, a, b=None, device=None):
+    """pp_libm_eval: the kernels' restated glibc sin/cos/atan2 (csrc/pp_glibcm.h) over a float64
+    array; numpy arrays run the host build, torch CUDA tensors the device build."""
+    k = LIBM_KINDS[kind]
+    if device is None:
+        a = np.ascontiguousarray(a, np.float64)
+        b = np.ascontiguousarray(b if b is not None else a, np.float64)
+        out = np.empty_like(a)
+        _check(lib.pp_libm_eval(k, a.ctypes.data, b.ctypes.data, out.ctypes.data, a.size, -1, None), "pp_libm_eval")
+        return out
+    import torch
+    b = b if b is not None else a
+    out = torch.empty_like(a)
+    st = torch.cuda.current_stream(device).cuda_stream
+    _check(lib.pp_libm_eval(k, a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), device, st), "pp_libm_eval")
+    return out
 
 
 # ---- wire codec (include/pp.h pp_telemetry_parse / pp_control_format; host) ----------------------

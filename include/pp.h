@@ -363,6 +363,15 @@ int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches
  * 0x4D43}), scaled to unit variance: only exactly rounded arithmetic, no libm. */
 double  pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q);
 
+/* The reference's libm as the kernels compute it (csrc/pp_glibcm.h: glibc 2.35 x86-64 sin, cos,
+ * atan2 restated bit for bit; used for the frame's heading and rotations in k_prep, the device
+ * Map::Init and the scene generator). Evaluates out[i] = sin(a[i]) (kind 0), cos(a[i]) (kind 1) or
+ * atan2(a[i], b[i]) (kind 2) for i < n on `device` (pointers to device memory, on `hip_stream`),
+ * or on the host (device = -1, host pointers). sin/cos outside |x| < 105414350 give NaN. For
+ * parity tests of the device build against the host libm. */
+int32_t pp_libm_eval(int32_t kind, const double* a, const double* b, double* out, int64_t n,
+                     int32_t device, void* hip_stream);
+
 /* Library version / build info string. */
 const char* pp_version(void);
 

@@ -1037,6 +1037,13 @@ int ppo_eval(const double* wx, const double* wy, int n_wp, const pp_scene_batch*
 
 int ppo_num_lanes(void) { return PP_NUM_LANES; }
 
+/* glibc's own sin/cos/atan2 over arrays (kind 0/1/2), each its own libm call (this file is built
+ * with -fno-builtin-sin/-cos, as the reference's -O0 build never fuses them into sincos): the
+ * checker for pp_libm_eval (csrc/pp_glibcm.h). */
+void ppo_libm_batch(int kind, const double* a, const double* b, double* out, int64_t n) {
+    for (int64_t i = 0; i < n; i++) out[i] = kind == 0 ? sin(a[i]) : kind == 1 ? cos(a[i]) : atan2(a[i], b[i]);
+}
+
 int ppo_struct_sizes(int64_t* out4) {
     out4[0] = sizeof(pp_scene_batch);
     out4[1] = sizeof(pp_params);

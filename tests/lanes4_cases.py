@@ -6,7 +6,7 @@ in a child process whose environment selects the PP_NUM_LANES=4 builds:
                  compiled with NUM_LANES 4: src/main.cpp:23-1154 after -DNUM_LANES=4)
 The reference makes NUM_LANES a compile-time constant (src/main.cpp:22); every array, loop and
 candidate count follows it, and so do ours. Same bars as the 3-lane suites: the restatement equals
-the reference bit for bit; the HIP path is within 1e-6 m (test_gpu_parity.compare)."""
+the reference bit for bit; the HIP path is within 1e-6 m (oracle_lib.compare)."""
 import numpy as np
 import pytest
 
@@ -104,7 +104,7 @@ class TestFourLanesGPU:
         md = ppamd.Map.from_device(wx, wy, device=0)
         a, b = md.geometry(), env["m"].geometry()
         assert a.shape == b.shape == (len(env["wx"]), 12)
-        assert np.abs(a - b).max() <= 1e-9
+        assert np.array_equal(a, b)          # pp_glibcm.h on the device: bit for bit
 
     def test_gpu_rollout_vs_restatement(self, env):
         t = env["torch"]

@@ -46,6 +46,7 @@ def load_oracle():
                                 C.POINTER(ppamd.RolloutLog)]
     lib.ppo_rollout.restype = C.c_int
     lib.ppo_num_lanes.restype = C.c_int
+    lib.ppo_libm_batch.argtypes = [C.c_int, _dp, _dp, _dp, C.c_int64]
     assert lib.ppo_num_lanes() == ppamd.NUM_LANES, (ORACLE_SO, ppamd.LIB_PATH)
     return lib
 
@@ -230,3 +231,55 @@ def ref_json_dump(lib, x, y):
     n = lib.ref_json_dump(x.ctypes.data_as(_dp), y.ctypes.data_as(_dp), len(x), buf, cap)
     assert 0 < n <= cap
     return buf.raw[:n]
+
+
+# ------------------------------------------------------------------------------------------------
+# the parity contract (north_star): HIP result vs the oracle on the same scenes
+# ------------------------------------------------------------------------------------------------
+TOL = 1e-6        # max |dxy| per point, metres
+
+
+def max_err(a, b):
+    """Largest |a - b| over finite values; the NaN pattern must be identical."""
+    fa, fb = np.isfinite(a), np.isfinite(b)
+    assert (fa == fb).all(), f"NaN pattern differs at {np.count_nonzero(fa != fb)} values"
+    return float(np.abs(a[fa] - b[fa]).max()) if fa.any() else 0.0
+
+
+def compare(got, ref, check_cost=True):
+    """Strict parity of a pp_eval result with the oracle's: winners, output counts, path lengths
+    and status words exact; every path point and next_x/next_y within TOL with an identical NaN
+    pattern (the reference's standstill 0/0 NaN, src/main.cpp:1025, included: pp_glibcm.h makes
+    the frame's trig the reference's libm bit for bit, so both sides take the same branch);
+    costs within 1e-9. Returns the largest |dxy|."""
+    S, Cn = got["cost"].shape
+    e = 0.0
+    if "paths" in ref:
+        assert (got["path_len"] == ref["path_len"]).all(), \
+            f"path_len differs for {int((got['path_len'] != ref['path_len']).sum())} candidates"
+        e = max_err(got["paths"], ref["paths"])
+        assert e <= TOL, e
+    assert (got["winner"] == ref["winner"]).all(), f"winner differs in {int((got['winner'] != ref['winner']).sum())} scenes"
+    assert (got["n_out"] == ref["n_out"]).all()
+    N = got["next_x"].shape[0]          # next_x/next_y are point-major [N][S]
+    live = np.arange(N)[:, None] < got["n_out"][None, :]
+    for k in ("next_x", "next_y"):
+        ee = max_err(np.where(live, got[k], 0.0), np.where(live, ref[k], 0.0))
+        assert ee <= TOL, (k, ee)
+        e = max(e, ee)
+    if check_cost:
+        np.testing.assert_allclose(got["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert (got["status"] == ref["status"].view(np.uint32)).all(), \
+        f"status differs in {int((got['status'] != ref['status'].view(np.uint32)).sum())} scenes"
+    return e
+
+
+def glibc_batch(olib, kind, a, b=None):
+    """glibc's own sin/cos/atan2 (kind 'sin'/'cos'/'atan2') over float64 arrays, one libm call
+    per element (oracle/pp_oracle.c ppo_libm_batch)."""
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b if b is not None else a, np.float64)
+    out = np.empty_like(a)
+    olib.ppo_libm_batch({"sin": 0, "cos": 1, "atan2": 2}[kind], a.ctypes.data_as(_dp), b.ctypes.data_as(_dp),
+                        out.ctypes.data_as(_dp), a.size)
+    return out

@@ -101,24 +101,19 @@ class TestMonteCarloGPU:
         return ppamd.result_to_numpy(r)
 
     def check(self, got, ref, D, Cv):
-        """Costs within 1e-9 (a few standstill-quirk candidates, see test_gpu_parity, may differ);
-        decisions exact where no cost differs; nominal trajectory within 1e-6 m; flags exact."""
+        """Costs within 1e-9, decisions and output counts exact, nominal trajectory within 1e-6 m,
+        flags exact: every scene, no allowance."""
+        np.testing.assert_allclose(got["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+        assert (got["winner"] == ref["winner"]).all()
+        np.testing.assert_allclose(got["draw_mean_cost"], ref["draw_mean_cost"], rtol=1e-9, atol=1e-9)
+        assert (got["n_out"] == ref["n_out"]).all()
         S = got["cost"].shape[0]
-        close = np.isclose(got["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
-        bad = ~close.all(1)
-        assert bad.sum() <= max(2, 1e-3 * S), int(bad.sum())
-        ok = ~bad
-        assert (got["winner"][ok] == ref["winner"][ok]).all()
-        np.testing.assert_allclose(got["draw_mean_cost"][ok], ref["draw_mean_cost"][ok], rtol=1e-9, atol=1e-9)
-        for s in np.nonzero(ok)[0]:
+        for s in range(S):
             n = ref["n_out"][s]
-            assert got["n_out"][s] == n, s
             e = max(np.abs(got["next_x"][:n, s] - ref["next_x"][:n, s]).max(initial=0),
                     np.abs(got["next_y"][:n, s] - ref["next_y"][:n, s]).max(initial=0))
             assert e <= 1e-6, (s, e)
-        nanb = np.uint32(ppamd.STATUS_BITS["NAN"])
-        m = np.where(bad, ~nanb, np.uint32(0xFFFFFFFF))
-        assert ((got["status"] & m) == (ref["status"].view(np.uint32) & m)).all()
+        assert (got["status"] == ref["status"].view(np.uint32)).all()
 
     @pytest.mark.parametrize("mode,n_speeds,D,S", [
         (ppamd.COST_REFERENCE, 1, 64, 384),     # BASELINE config 4 shape: 64 draws x 3 lanes
