@@ -2,16 +2,21 @@
 
 A step = one pp_eval over one resident batch of synthetic scenes (inputs already in HBM): K1 scene
 prep + K2 candidate evaluation (3 lanes x n_speeds, 50-point horizon, spline + limiter + cost)
-+ per-scene winner path. Default workload = BASELINE config 5's batch, 2,097,152 scenes x 15
-candidates per GPU (weak scaling: rank r evaluates global scenes [r*S, (r+1)*S) of one seeded
-synthetic stream; no collective on the data path, only the timing barrier + max).
++ the per-scene winner path. Default workload = BASELINE config 5: 2,097,152 scenes x 15
+candidates IN TOTAL, sharded over the N GPUs (strong scaling: rank r evaluates the contiguous
+global scenes [r S/N, (r+1) S/N) of one seeded synthetic stream). No collective on the data path:
+the ranks meet only in the timing barrier and the max over ranks, both over gloo on the host.
+For N > 1 the line also carries a weak-scaling measurement (2,097,152 scenes per GPU).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+Run: python bench.py [--gpus N --steps K --warmup W]. Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank; without it, --gpus N > 1 starts N rank processes itself (the parent
+never touches the GPU) and exits with their status.
 """
 import argparse
-import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,6 +28,7 @@ sys.path.insert(0, PKG)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 SCENE_BYTES = 4 * 8 + 20 * 8 + 3 * 4 + 12 * (4 + 4 * 8)   # SoA scene record (include/pp.h): 636 B
+CONFIG5_SCENES = 2_097_152
 
 
 def algorithmic_bytes_per_candidate(C_, N, emit_paths):
@@ -33,20 +39,54 @@ def algorithmic_bytes_per_candidate(C_, N, emit_paths):
     return (SCENE_BYTES + 8 + 16 * N) / C_ + 8
 
 
-def shard(rank, scenes_per_rank):
-    """Weak scaling: rank r owns global scenes [r*S, (r+1)*S) of one seeded synthetic stream
-    (pp_synth_scenes first_scene = r*S); scenes depend only on (seed, global index)."""
-    return rank * scenes_per_rank, scenes_per_rank
+def shard(rank, world, total=None, per_rank=None):
+    """Scene range (first, count) of `rank`. Strong scaling (total given): contiguous balanced
+    shards of `total` global scenes; weak scaling (per_rank given): [rank * per_rank, ...).
+    Scenes depend only on (seed, global index), so any layout evaluates the same scenes."""
+    if total is not None:
+        lo = rank * total // world
+        hi = (rank + 1) * total // world
+        return lo, hi - lo
+    return rank * per_rank, per_rank
 
 
-def max_over_ranks(elapsed, dist, device):
-    """The job's time is the slowest rank's (MAX all-reduce; RCCL on GPUs, gloo in the CPU test)."""
+def max_over_ranks(elapsed, dist, device=None):
+    """The job's time is the slowest rank's: MAX all-reduce of a host tensor over the gloo group."""
     if dist is None:
         return elapsed
     import torch
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rank_envs(n, port, base=None):
+    """Environments of the n rank processes the launcher starts (torch.distributed.run's names)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        envs.append(e)
+    return envs
+
+
+def launch(n, argv):
+    """Start n rank processes of this script (the parent has not touched the GPU) and wait for them;
+    rank 0 prints the JSON line. Returns the worst exit status."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e)
+             for e in rank_envs(n, free_port())]
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
 
 
 def load_valu_peak():
@@ -59,23 +99,23 @@ def load_valu_peak():
         return None, None
 
 
-def load_f64_instr(tag):
-    """FP64 VALU wave-instructions per k_cand launch from the committed PMC summary."""
+def load_pmc(tag):
+    """Per-launch counters of the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
-        c = json.load(open(p))[tag]["counters"]
-        return sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
-                                            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")), c.get("SQ_INSTS_VALU")
+        return json.load(open(p)).get(tag)
     except Exception:
-        return None, None
+        return None
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scenes", type=int, default=2_097_152, help="scenes per GPU")
+    ap.add_argument("--scenes", type=int, default=CONFIG5_SCENES,
+                    help="total scenes (strong scaling) or scenes per GPU (--scaling weak)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--n-speeds", type=int, default=5)
     ap.add_argument("--n-points", type=int, default=50)
     ap.add_argument("--emit-paths", action="store_true", help="write every candidate path (config 3)")
@@ -86,77 +126,165 @@ def parse():
                     help="closed-loop mode: one step = this many pp_rollout frames (plan + simulator)")
     ap.add_argument("--sensor-range", type=float, default=300.0)
     ap.add_argument("--seed", type=int, default=0x5EED0001)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline time budget per leg")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="all-core leg threads (0: the host's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
+    ap.add_argument("--cpu-ranks", action="store_true",
+                    help="launcher rehearsal without a GPU: every rank evaluates its shard with the CPU oracle")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(m, scenes_dev, prm, budget_s):
-    """Reference planning code (oracle/_ref, compiled from the reference's sources) if it was
-    built, else the C restatement (oracle/liboracle.so), on one host core over a bounded sample."""
+def host_cpu():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        share = min(share, int(omp))
+    return model, os.cpu_count(), max(1, min(share, 64))
+
+
+def cpu_baseline(scenes_host_fn, S, prm, budget_s, threads):
+    """The reference's own planning code (oracle/_ref, compiled from the reference's sources) if it
+    was built, else the C restatement (oracle/liboracle.so): one host core, then `threads` cores
+    (std::thread-like: Python threads around the GIL-free ctypes call, static chunk partition),
+    each leg over a bounded sample of the same synthetic batch."""
+    import threading
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib
     import ppamd
     wx, wy = ppamd.highway_map()
     rlib = oracle_lib.load_ref() if prm.n_points == 50 and not prm.emit_paths and prm.n_draws <= 1 else None
     olib = None if rlib else oracle_lib.load_oracle()
-    chunk = 2048
-    S = int(scenes_dev["ego_x"].shape[0])
-    done, t_used, start = 0, 0.0, 0
     offs = [prm.speed_offsets[i] for i in range(prm.n_speeds - 1)]
-    while t_used < budget_s and start < S:
-        host = {k: np.ascontiguousarray(v[..., start:start + chunk].cpu().numpy()) for k, v in scenes_dev.items()}
-        t0 = time.perf_counter()
+    chunk = 1024
+    cand_per_scene = 3 * prm.n_speeds * max(prm.n_draws, 1)
+
+    def run_chunk(host):
         if rlib:
             oracle_lib.ref_eval(rlib, wx, wy, host, prm.n_speeds, offs, with_frame=False)
         else:
             oracle_lib.oracle_eval(olib, wx, wy, host, prm, info=False)
-        t_used += time.perf_counter() - t0
-        done += host["ego_x"].shape[0]
-        start += chunk
-    cands = done * 3 * prm.n_speeds * max(prm.n_draws, 1)
-    return {"value": cands / t_used, "unit": "candidate trajectories/s", "cores": 1,
-            "kind": "reference" if rlib else "port",
-            "sample": f"first {done} scenes x {3 * prm.n_speeds * max(prm.n_draws, 1)} candidates of the same synthetic "
-                      f"batch ({t_used:.1f} s, single thread; "
-                      + ("reference src/main.cpp classes built by oracle/Makefile" if rlib else
-                         "C restatement oracle/pp_oracle.c") + ")"}
 
+    def leg(nthreads):
+        """Scenes done / wall time with nthreads workers pulling chunks until the budget ends."""
+        lock = threading.Lock()
+        state = {"next": 0, "done": 0}
+        t0 = time.perf_counter()
 
-def load_traffic(tag):
-    """Per-launch HBM bytes of k_cand from the committed rocprofv3 PMC summary (profiles/)."""
-    p = os.path.join(REPO, "profiles", "pmc_summary.json")
-    if not os.path.exists(p):
-        return None, None
+        def worker():
+            while True:
+                with lock:
+                    if time.perf_counter() - t0 > budget_s or state["next"] >= S:
+                        return
+                    start = state["next"]
+                    state["next"] += chunk
+                host = scenes_host_fn(start, min(chunk, S - start))
+                run_chunk(host)
+                with lock:
+                    state["done"] += host["ego_x"].shape[0]
+
+        ts = [threading.Thread(target=worker) for _ in range(nthreads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return state["done"], time.perf_counter() - t0
+
+    # the reference's printf warnings ("detected collision", "spline input error") go to fd 1: keep
+    # them out of the bench's one-line JSON stdout
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
     try:
-        d = json.load(open(p))
-        e = d.get(tag)
-        if not e:
-            return None, None
-        return e["hbm_bytes_per_launch"], e.get("source")
-    except Exception:
-        return None, None
+        d1, t1 = leg(1)
+        dn, tn = leg(threads) if threads > 1 else (d1, t1)
+    finally:
+        import ctypes
+        ctypes.CDLL(None).fflush(None)           # C stdio buffers drain into /dev/null too
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
+    model, nproc, _ = host_cpu()
+    src = "reference src/main.cpp classes built by oracle/Makefile" if rlib else "C restatement oracle/pp_oracle.c"
+    return {"value": dn * cand_per_scene / tn, "unit": "candidate trajectories/s", "cores": threads,
+            "kind": "reference" if rlib else "port",
+            "value_1core": d1 * cand_per_scene / t1, "nproc": nproc, "cpu_model": model,
+            "sample": f"{dn} scenes x {cand_per_scene} candidates of the same synthetic batch on {threads} "
+                      f"threads ({tn:.1f} s), and {d1} scenes on 1 thread ({t1:.1f} s); {src}"}
 
 
-def main():
-    a = parse()
-    import torch
+def run_cpu_ranks(a, rank, world, dist):
+    """--cpu-ranks: the launcher, sharding and timing protocol rehearsed without a GPU (CPU oracle)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
     import ppamd
+    wx, wy = ppamd.highway_map()
+    m = ppamd.Map(wx, wy)
+    olib = oracle_lib.load_oracle()
+    prm = ppamd.default_params(n_speeds=a.n_speeds)
+    first, n = shard(rank, world, total=a.scenes) if a.scaling == "strong" else shard(rank, world, per_rank=a.scenes)
+    sc = ppamd.synth_host(m, n, seed=a.seed, first=first)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        r = oracle_lib.oracle_eval(olib, wx, wy, sc, prm, info=False)
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist)
+    digest = float(np.nansum(r["cost"]))
+    digests = [digest]
+    shards = [(first, n)]
+    if dist:
+        digests = [None] * world
+        shards = [None] * world
+        dist.all_gather_object(digests, digest)
+        dist.all_gather_object(shards, (first, n))
+    total = sum(c for _, c in shards)
+    return {"metric": "candidate trajectories/sec (CPU rehearsal of the rank launcher)", "value":
+            total * 3 * a.n_speeds * a.steps / elapsed, "n_gpus": world, "steps": a.steps,
+            "scaling": a.scaling, "shards": shards, "cost_digests": digests, "ms_per_step": elapsed / a.steps * 1e3}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return launch(a.gpus, argv)
+    world = int(env_world or "1")
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.cpu_ranks:
+        out = run_cpu_ranks(a, rank, world, dist)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return 0
+
+    import torch
+    import ppamd
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-
     wx, wy = ppamd.highway_map()
     m = ppamd.Map(wx, wy)
-    S = a.scenes
     prm = ppamd.default_params(n_speeds=a.n_speeds, n_points=a.n_points,
                                cost_mode=ppamd.COST_COMFORT if a.comfort else ppamd.COST_REFERENCE,
                                emit_paths=a.emit_paths, n_draws=a.draws, noise_first_scene=0,
@@ -165,100 +293,151 @@ def main():
     Cn = D * 3 * a.n_speeds
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-    m.reserve(local, S * D)
-    first, _ = shard(rank, S)
-    prm.noise_first_scene = first
-    traffic = None
-    if a.rollout:
-        scenes, traffic = ppamd.synth_traffic(m, S, seed=a.seed, first=first, device=local, stream=sp)
-    else:
-        scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
-    res = ppamd.alloc_result(S, prm, xp="torch", device=dev)
-    torch.cuda.synchronize(dev)
-
-    def step():
-        if a.rollout:
-            ppamd.rollout(m, scenes, traffic, prm, res, a.rollout, 3, a.sensor_range, device=local, stream=sp)
-        else:
-            ppamd.evaluate(m, scenes, prm, res, device=local, stream=sp)
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    m.timing(local, True)
-    m.read_timing(local)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ms, launches = m.read_timing(local)
-    m.timing(local, False)
-    elapsed = max_over_ranks(elapsed, dist, dev)
     frames = max(a.rollout, 1)
-    total_cands = S * Cn * world * a.steps * frames
-    value = total_cands / elapsed
-    # dominant kernel: k_cand (HIP events on the launch stream, timed region only)
-    k_cand_ms = ms[1] / max(launches[1], 1)      # per launch (one frame)
+
+    def measure(first, S, steps, warmup):
+        """One timed run over this rank's shard: W untimed steps, then K steps bracketed by a
+        barrier + device synchronisation on both sides; returns (max-over-ranks seconds, per-kernel
+        ms and launches of this rank, the resident scenes)."""
+        m.reserve(local, S * D)
+        p = ppamd.default_params(n_speeds=a.n_speeds, n_points=a.n_points,
+                                 cost_mode=prm.cost_mode, emit_paths=a.emit_paths, n_draws=a.draws,
+                                 noise_first_scene=first,
+                                 speed_offsets=[-6, -4, -3, -2, -1, 0, 2] if a.n_speeds == 8 else None)
+        traffic = None
+        if a.rollout:
+            scenes, traffic = ppamd.synth_traffic(m, S, seed=a.seed, first=first, device=local, stream=sp)
+        else:
+            scenes = ppamd.synth_device(m, S, seed=a.seed, first=first, device=local, stream=sp)
+        res = ppamd.alloc_result(S, p, xp="torch", device=dev)
+        torch.cuda.synchronize(dev)
+
+        def step():
+            if a.rollout:
+                ppamd.rollout(m, scenes, traffic, p, res, a.rollout, 3, a.sensor_range, device=local, stream=sp)
+            else:
+                ppamd.evaluate(m, scenes, p, res, device=local, stream=sp)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        m.timing(local, True)
+        m.read_timing(local)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        ms, launches = m.read_timing(local)
+        m.timing(local, False)
+        del res
+        return max_over_ranks(elapsed, dist), ms, launches, scenes
+
+    if a.scaling == "strong":
+        first, S = shard(rank, world, total=a.scenes)
+        total_scenes = a.scenes
+    else:
+        first, S = shard(rank, world, per_rank=a.scenes)
+        total_scenes = a.scenes * world
+    elapsed, ms, launches, scenes = measure(first, S, a.steps, a.warmup)
+    value = total_scenes * Cn * a.steps * frames / elapsed
+    # per-rank kernel times (HIP events on each rank's launch stream, timed region only)
+    kms = {"rank": rank, "scenes": S, "k_prep": ms[0] / max(launches[0], 1), "k_cand": ms[1] / max(launches[1], 1),
+           "k_out": (ms[2] / launches[2]) if launches[2] else None}
+    per_rank = [kms]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, kms)
+    weak = None
+    if world > 1 and not a.no_weak and a.scaling == "strong":
+        del scenes
+        torch.cuda.empty_cache()
+        wfirst, wS = shard(rank, world, per_rank=CONFIG5_SCENES)
+        wel, _, _, scenes = measure(wfirst, wS, a.steps, a.warmup)
+        weak = {"value": wS * world * Cn * a.steps * frames / wel, "scenes_per_gpu": wS,
+                "ms_per_step": wel / a.steps * 1e3}
+    # dominant kernel: k_cand on this rank
+    k_cand_ms = kms["k_cand"]
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
-    bytes_launch = bpc * S * Cn
-    achieved = bytes_launch / (k_cand_ms * 1e-3) / 1e9
-    tag = f"k_cand_S{S}_C{Cn}_N{a.n_points}" + ("_paths" if a.emit_paths else "") + (f"_D{D}" if D > 1 else "")
-    traffic, traffic_src = load_traffic(tag)
+    cands_launch = S * Cn
+    achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
+    tag = f"k_cand_S{CONFIG5_SCENES if not (a.emit_paths or D > 1) else S}_C{Cn}_N{a.n_points}" + \
+        ("_paths" if a.emit_paths else "") + (f"_D{D}" if D > 1 else "")
+    pmc = load_pmc(tag)
+    traffic = traffic_pipe = None
+    if pmc:
+        # per-candidate counter bytes of the profiled launch, scaled to this launch
+        pc = pmc.get("candidates_per_launch") or (CONFIG5_SCENES * Cn)
+        traffic = pmc["hbm_bytes_per_launch"] / pc * cands_launch
+        if pmc.get("pipeline_bytes_per_step"):
+            traffic_pipe = pmc["pipeline_bytes_per_step"] / pc * cands_launch
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",
         "value": value, "unit": "candidate trajectories/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": a.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (Philox scenes on highway_map.csv, seeded; SURVEY.md §8(d))",
-        "config": {"workload": (f"BASELINE config 4: {S} scenes x {D} sensor-noise draws x 3 lanes x "
+        "config": {"workload": (f"BASELINE config 4: {total_scenes} scenes x {D} sensor-noise draws x 3 lanes x "
                                 f"{a.n_speeds} speeds, per-scene argmin over draws" if D > 1 else
-                                f"BASELINE config 5 batch: {S} scenes x 3 lanes x {a.n_speeds} speeds")
-                               + f", {a.n_points}-pt horizon per GPU"
+                                f"BASELINE config 5: {total_scenes} scenes x 3 lanes x {a.n_speeds} speeds")
+                               + (f" sharded over {world} GPUs" if a.scaling == "strong" else f" ({S} per GPU)")
+                               + f", {a.n_points}-pt horizon"
                                + (", all paths emitted" if a.emit_paths else ", winner path + costs")
                                + (f", closed loop: {a.rollout} frames per step (plan + simulator, 3 points "
                                   f"driven per frame, sensor range {a.sensor_range:g} m)" if a.rollout else "")
                                + (", comfort cost" if a.comfort else ", reference decision"),
-                   "scenes_per_gpu": S, "candidates_per_scene": Cn, "horizon_points": a.n_points,
-                   "parallelism": f"scene shards x{world}, no collective"},
-        "kernels_ms_avg": {"k_prep": ms[0] / max(launches[0], 1), "k_cand": k_cand_ms,
-                           "k_out": (ms[2] / launches[2]) if launches[2] else None},
+                   "scenes_total": total_scenes, "scenes_per_gpu": S, "candidates_per_scene": Cn,
+                   "horizon_points": a.n_points,
+                   "parallelism": f"contiguous scene shards x{world}, no collective (gloo barrier + max for timing)"},
+        "kernels_ms_avg": {k: kms[k] for k in ("k_prep", "k_cand", "k_out")},
+        "per_rank_kernels_ms": per_rank,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_cand", "algorithmic_bytes_per_candidate": bpc,
-                     "traffic_source": traffic_src},
+                     "traffic_pipeline": traffic_pipe,
+                     "traffic_source": (pmc or {}).get("source")},
     }
-    # the bound that matters for this path: FP64 VALU issue (no MFMA-shaped work, HBM ~3 %)
-    f64, allv = load_f64_instr(tag)
+    if weak:
+        out["weak_scaling"] = weak
+    # the bound that matters for this path: FP64 VALU issue (no MFMA-shaped work, HBM a few %)
     peak, peak_add = load_valu_peak()
-    if f64 and peak:
+    if pmc and peak:
+        c = pmc["counters"]
+        pc = pmc.get("candidates_per_launch") or (CONFIG5_SCENES * Cn)
+        f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                           "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")) / pc * cands_launch
+        allv = c.get("SQ_INSTS_VALU", 0.0) / pc * cands_launch
         ach = f64 / (k_cand_ms * 1e-3)
         out["valu_roofline"] = {"bound": "fp64-valu-issue", "kernel": "k_cand",
                                 "achieved_f64_wave_instr_per_s": ach, "peak_f64_fma_wave_instr_per_s": peak,
                                 "frac": ach / peak, "all_valu_wave_instr_per_launch": allv,
                                 "f64_wave_instr_per_launch": f64,
-                                "source": "rocprofv3 PMC SQ_INSTS_VALU_*_F64 per launch (profiles/pmc_summary.json) "
-                                          "/ this run's k_cand time; peak measured by tools/valu_peak.hip"}
-        if allv and peak_add:
-            # every VALU instruction (FP64, int, moves, compares) against the fastest measured
-            # single-instruction issue rate (v_add_f64): the share of the VALU issue slots used
-            out["valu_roofline"]["all_valu_wave_instr_per_s"] = allv / (k_cand_ms * 1e-3)
-            out["valu_roofline"]["peak_issue_wave_instr_per_s"] = peak_add
-            out["valu_roofline"]["issue_frac"] = allv / (k_cand_ms * 1e-3) / peak_add
+                                "all_valu_wave_instr_per_s": allv / (k_cand_ms * 1e-3),
+                                "peak_issue_wave_instr_per_s": peak_add,
+                                "issue_frac": allv / (k_cand_ms * 1e-3) / peak_add if peak_add else None,
+                                "source": "rocprofv3 PMC SQ_INSTS_VALU_* per candidate (profiles/pmc_summary.json) "
+                                          "x this launch's candidates / this run's k_cand time; peak measured by "
+                                          "tools/valu_peak.hip"}
     if a.rollout:
-        out["scene_frames_per_s"] = S * world * a.steps * frames / elapsed
+        out["scene_frames_per_s"] = total_scenes * a.steps * frames / elapsed
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
-        out["cpu_baseline"] = cpu_baseline(m, scenes, prm, a.cpu_seconds)
+        model, nproc, share = host_cpu()
+        threads = a.cpu_threads or share
+
+        def scenes_host(start, n):
+            return {k: np.ascontiguousarray(v[..., start:start + n].cpu().numpy()) for k, v in scenes.items()}
+        out["cpu_baseline"] = cpu_baseline(scenes_host, S, prm, a.cpu_seconds, threads)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -29,7 +29,7 @@ def _worker(rank, world, port, out_dir):
     import bench
     wx, wy = ppamd.highway_map()
     m = ppamd.Map(wx, wy)
-    first, n = bench.shard(rank, S_PER_RANK)
+    first, n = bench.shard(rank, world, per_rank=S_PER_RANK)
     sc = ppamd.synth_host(m, n, seed=99, first=first)
     prm = ppamd.default_params()
     r = oracle_lib.oracle_eval(oracle_lib.load_oracle(), wx, wy, sc, prm, info=False)
@@ -39,7 +39,7 @@ def _worker(rank, world, port, out_dir):
     gn = [torch.zeros_like(nxt) for _ in range(world)]
     dist.all_gather(gc, cost)
     dist.all_gather(gn, nxt)
-    t = bench.max_over_ranks(1.0 + rank, dist, torch.device("cpu"))
+    t = bench.max_over_ranks(1.0 + rank, dist)
     if rank == 0:
         np.savez(os.path.join(out_dir, "dist.npz"), cost=torch.cat(gc).numpy(),
                  next_x=torch.cat(gn).numpy(), t=t)
@@ -58,3 +58,43 @@ def test_two_rank_shards_equal_single_process(tmp_path):
     r = oracle_lib.oracle_eval(oracle_lib.load_oracle(), wx, wy, full, ppamd.default_params(), info=False)
     assert np.array_equal(z["cost"], r["cost"])
     assert np.array_equal(z["next_x"], r["next_x"].T)
+
+
+def test_shard_arithmetic():
+    """Strong scaling (BASELINE config 5: 2,097,152 scenes in total) and weak scaling shards for
+    1/2/4/8 GPUs: contiguous, disjoint, covering, balanced."""
+    import bench
+    for G in (1, 2, 4, 8):
+        sh = [bench.shard(r, G, total=bench.CONFIG5_SCENES) for r in range(G)]
+        assert sh[0][0] == 0 and sum(n for _, n in sh) == bench.CONFIG5_SCENES
+        assert all(sh[i][0] + sh[i][1] == sh[i + 1][0] for i in range(G - 1))
+        assert {n for _, n in sh} == {bench.CONFIG5_SCENES // G}
+        w = [bench.shard(r, G, per_rank=1000) for r in range(G)]
+        assert w == [(1000 * r, 1000) for r in range(G)]
+    odd = [bench.shard(r, 3, total=10) for r in range(3)]
+    assert odd == [(0, 3), (3, 3), (6, 4)]
+    envs = bench.rank_envs(4, 12345, base={})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"] and all(e["WORLD_SIZE"] == "4" for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" for e in envs)
+
+
+def test_launcher_starts_n_ranks():
+    """`bench.py --gpus 4` without torchrun starts 4 rank processes (gloo barrier + max); the CPU
+    rehearsal evaluates each rank's shard with the oracle and reports n_gpus = 4 over the whole
+    batch, equal to a single-process evaluation."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(oracle_lib.REPO, "bench.py"), "--gpus", "4", "--cpu-ranks",
+                        "--scenes", "66", "--steps", "1"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 4 and out["scaling"] == "strong"
+    assert [tuple(x) for x in out["shards"]] == [(0, 16), (16, 17), (33, 16), (49, 17)]
+    wx, wy = ppamd.highway_map()
+    m = ppamd.Map(wx, wy)
+    full = oracle_lib.oracle_eval(oracle_lib.load_oracle(), wx, wy, ppamd.synth_host(m, 66, seed=0x5EED0001, first=0),
+                                  ppamd.default_params(), info=False)
+    parts = [float(np.nansum(full["cost"][f:f + n])) for f, n in out["shards"]]
+    assert np.allclose(parts, out["cost_digests"], rtol=1e-12)
