@@ -19,11 +19,13 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <new>
 #include <vector>
 
 #include "../../include/pp.h"
+#include "pp_cartable.h"
 #ifdef PP_DIAG
 // diagnostic builds only (-DPP_DIAG): per event, [2k] lanes where it fired, [2k+1] waves where any
 // lane fired (the wave executes the branch). Read with pp_diag_read.
@@ -140,9 +142,12 @@ __device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_
         vy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, it, 3);
     }
 }
+// k_cand groups (SPB scenes per group, or BPS groups per scene): k_prep marks the groups holding a
+// kLimSlow scene in this bitmap for k_cand<true>
+struct GroupBits { uint32_t* bits; int SPB, BPS; };
 template <bool kLdsMap>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_scene_info* info, uint32_t* out_status) {
+                                              pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
     if (kLdsMap) {
@@ -220,14 +225,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
     // Without a car table: the frame's rows in order (ascending ids). With one (the reference's
-    // persistent std::map): ids 0..PP_MAX_CARS-1 in order, each either reported this frame
-    // (re-matched; slot overwritten, or erased when matching fails, src/main.cpp:1329-1348) or
-    // taken from its stale slot.
+    // persistent std::map): its tab_slots slots in order (ascending ids, include/pp.h), each car
+    // either reported this frame (re-matched; slot overwritten, or erased when matching fails,
+    // src/main.cpp:1329-1348) or taken from its stale slot.
     const bool tab = in.tab_valid != nullptr;
 #ifdef PP_ABL_PREP_NOCARS   // diagnostic timing build: ego only
     const int iters = 0;
 #else
-    const int iters = tab ? PP_MAX_CARS : ncar;
+    const int iters = tab ? in.tab_slots : ncar;
 #endif
     // Visiting order. Every per-car reduction below is a minimum with ties to the lower iteration
     // index (or an AND / a count), so any visiting order gives the reference's result once ties
@@ -236,13 +241,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // sorted by a Batcher network): the k-th visit of every lane of a wave then walks a similar
     // number of lane segments in lane_matching, which is where the divergence was. With a table,
     // or a negative car id (the reference's -1 'no car' sentinel), the identity order is kept.
+    // (more than 16 rows: the identity order)
     uint64_t order = 0xFEDCBA9876543210ull;
+    bool sorted = false;
 #if PP_CAR_SORT
-    if (!tab && iters > 1) {
-        uint32_t key[PP_MAX_CARS];
+    if (!tab && iters > 1 && iters <= 16) {
+        uint32_t key[16];
         bool neg = false;
 #pragma unroll
-        for (int j = 0; j < PP_MAX_CARS; j++) {
+        for (int j = 0; j < 16; j++) {
             key[j] = 0xFFFFFFF0u | (uint32_t)j;
             if (j < iters) {
                 const int64_t ix = (int64_t)j * S + s;
@@ -253,11 +260,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             }
         }
 #pragma unroll
-        for (int pw = 1; pw < PP_MAX_CARS; pw <<= 1)
+        for (int pw = 1; pw < 16; pw <<= 1)
 #pragma unroll
             for (int k = pw; k >= 1; k >>= 1)
 #pragma unroll
-                for (int j = k % pw; j < PP_MAX_CARS - k; j += 2 * k)
+                for (int j = k % pw; j < 16 - k; j += 2 * k)
 #pragma unroll
                     for (int i = 0; i < k; i++)
                         if ((i + j) / (2 * pw) == (i + j + k) / (2 * pw)) {
@@ -268,28 +275,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         if (!neg) {
             order = 0;
 #pragma unroll
-            for (int j = 0; j < PP_MAX_CARS; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
+            for (int j = 0; j < 16; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
+            sorted = true;
         }
     }
 #endif
-    // iteration index of each running minimum, 4 bits each: next_s[l] at 4 l, the target-lane car
-    // of lane l at 4 (NL + l), the in-lane car at 8 NL (the follow cars' velocities are re-read
-    // from that index after the pass)
+    // iteration index of each running minimum, 6 bits each: next_s[l] at field l, the target-lane
+    // car of lane l at field NL + l, the in-lane car at field 2 NL (the follow cars' velocities are
+    // re-read from that index after the pass)
+    static_assert((2 * NL + 1) * 6 <= 64 && PP_MAX_CARS <= 64, "iteration index fields");
     uint64_t its = 0;
-    auto it_of = [&](int f) { return (int)((its >> (4 * f)) & 15); };
-    auto set_it = [&](int f, int it) { its = (its & ~(15ull << (4 * f))) | ((uint64_t)it << (4 * f)); };
+    auto it_of = [&](int f) { return (int)((its >> (6 * f)) & 63); };
+    auto set_it = [&](int f, int it) { its = (its & ~(63ull << (6 * f))) | ((uint64_t)it << (6 * f)); };
     int p = 0;                              // next unread row (table mode)
     for (int kk = 0; kk < iters; kk++) {
-        const int it = (int)((order >> (4 * kk)) & 15);
+        const int it = sorted ? (int)((order >> (4 * kk)) & 15) : kk;
         int row = it;
+        const int64_t tix = (int64_t)it * S + s;
+        // table mode: slot `it` holds car id sid (slots in ascending id order, include/pp.h)
+        const int sid = tab ? (in.tab_id ? in.tab_id[tix] : it) : 0;
         if (tab) {
-            while (p < ncar && in.car_id[(int64_t)p * S + s] < it) p++;     // ids must ascend
-            row = (p < ncar && in.car_id[(int64_t)p * S + s] == it) ? p++ : -1;
+            while (p < ncar && in.car_id[(int64_t)p * S + s] < sid) p++;    // ids must ascend
+            row = (p < ncar && in.car_id[(int64_t)p * S + s] == sid) ? p++ : -1;
         }
         int id;
         double cx, cy, cvx, cvy, cs, cd, cvs, cvd;
         int clane = 0;
-        const int64_t tix = (int64_t)it * S + s;
         if (row >= 0) {
             const int64_t ix = (int64_t)row * S + s;
             id = in.car_id[ix];
@@ -324,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             }
         } else {
             if (!in.tab_valid[tix]) continue;
-            id = it;
+            id = sid;
             clane = in.tab_lane[tix];
             cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
             cvx = in.tab_vx[tix]; cvy = in.tab_vy[tix];
@@ -423,7 +434,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     // LimitSpeed for the in-lane car and the per-lane target car (src/main.cpp:1411-1438)
     int lim_mask = 0;
     bool col;
-    if (in_id >= 0) {
+    // the reference's "no car" is id -1 (src/main.cpp:1383-1432): a chosen car whose id is -1
+    // reads as none; ids are what :1411 compares
+    if (in_id != -1) {
         double ts, tt;
         double in_vx, in_vy;
         car_velocity(in, P, S, s, draw, tab, it_of(2 * NL), in_vx, in_vy);
@@ -434,7 +447,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     }
 #pragma unroll
     for (int L = 0; L < NL; L++) {
-        if (t_id[L] >= 0 && t_id[L] != in_id) {
+        if (t_id[L] != -1 && t_id[L] != in_id) {
             double ts, tt;
             double t_vx, t_vy;
             car_velocity(in, P, S, s, draw, tab, it_of(NL + L), t_vx, t_vy);
@@ -469,6 +482,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         for (int L = 0; L < NL; L++)
             if (lim_mask & (2 << L)) ok = ok && speed_in_range(pv.l_ts[L * Sv + v]) && speed_in_range(pv.l_tt[L * Sv + v]);
         if (!ok) lim_mask |= kLimSlow;
+    }
+    if (lim_mask & kLimSlow) {
+        const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
+        for (int b = 0; b < gb.BPS; b++) atomicOr(&gb.bits[(g0 + b) >> 5], 1u << ((g0 + b) & 31));
     }
     pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
     // the frame's rotations cos(-angle), sin(-angle) (:786-787) and cos(angle), sin(angle)
@@ -1201,10 +1218,13 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 #ifndef PP_CAND_WAVES
 #define PP_CAND_WAVES 4
 #endif
+// One group g of the candidate grid (BPS == 1: scenes [g SPB, g SPB + SPB); BPS > 1: candidates
+// [coff, coff + 256) of scene g / BPS) by the whole workgroup. Every barrier inside is reached by
+// all threads of the block (the early return is block-uniform).
 template <bool kSlow, int kMode>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+__device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
+                                           const PrepV& pv, const pp_result& out, int SPB, int BPS,
+                                           double* rec, uint64_t* adjm, int64_t g, double* sm) {
     const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int C = D * Cv;                     // candidates per scene (all draws)
@@ -1223,8 +1243,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
     // [coff, coff + 256) of it
     int64_t s0;
     int coff;
-    if (BPS == 1) { s0 = (int64_t)blockIdx.x * SPB; coff = 0; }
-    else { s0 = blockIdx.x / BPS; coff = (int)(blockIdx.x - s0 * BPS) * 256; }
+    if (BPS == 1) { s0 = g * SPB; coff = 0; }
+    else { s0 = g / BPS; coff = (int)(g - s0 * BPS) * 256; }
     const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
     const int tid = threadIdx.x;
     // per scene: any of its draws flagged kLimSlow (absurd heading, or a speed or ramp time outside
@@ -1391,6 +1411,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAV
         const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
         if (BPS == 1) out.status[s0 + tid] = st;
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
+    }
+}
+
+// k_cand<false>: the full grid, one group per workgroup; scenes k_prep flagged kLimSlow are left
+// to k_cand<true>, which runs only the groups whose bit k_prep set in `gbits` (a bitmap over the
+// groups): gridDim.x workgroups walk the bitmap with stride gridDim.x (the bit test and the loop
+// are block-uniform; a barrier separates consecutive groups' use of the block's LDS). Each group
+// clears its bit after use, so the bitmap is all zero again for the next pp_eval.
+template <bool kSlow, int kMode>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+                                              pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
+                                              uint32_t* gbits, int64_t ngroups) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (!kSlow) {
+        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm);
+        return;
+    }
+    for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        const uint32_t word = gbits[g >> 5];                      // same address for every lane
+        if (!((word >> (g & 31)) & 1u)) continue;
+        __syncthreads();                                          // the previous group's LDS readers are done
+        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
+        if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
 
@@ -1674,8 +1717,10 @@ __global__ __launch_bounds__(256) void k_synth_traffic(ppsynth::LaneTables T, ui
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= o.S) return;
     ppsynth::synth_scene(T, seed, first + s, s, o, &tr);
-    if (tb.tab_valid)
-        for (int j = 0; j < PP_MAX_CARS; j++) tb.tab_valid[(int64_t)j * o.S + s] = 0;
+    for (int j = 0; tb.tab_valid && j < tb.tab_slots; j++) {       // empty table, slot j = car j
+        tb.tab_valid[(int64_t)j * o.S + s] = 0;
+        if (tb.tab_id) tb.tab_id[(int64_t)j * o.S + s] = j;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1770,23 +1815,28 @@ constexpr int kMaxWaypoints = 1 << 24;
 constexpr int kPrepD = 12 + 4 * NL;   // doubles per scene in PrepV (see prep_bind)
 constexpr int kPrepI = 7;
 
-struct DevState {
-    bool init = false;
-    double* map = nullptr;        // kMapArrays * n
-    double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
+// pp_eval's device workspaces, one set per HIP stream: evaluations on different streams never
+// share intermediate buffers, and evaluations on one stream are ordered by it. A buffer is grown
+// only after that stream has drained (it is the only stream using it).
+struct StreamWS {
     void* ws = nullptr;           // prep workspace (per evaluation: scene x draw)
     int64_t ws_cap = 0;
     void* rec = nullptr;          // reference-mode winner record (per scene)
     int64_t rec_cap = 0;
+    uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
+    int64_t gbits_cap = 0;        // words
+};
+struct DevState {
+    bool init = false;
+    double* map = nullptr;        // kMapArrays * n
+    double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
+    std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
+    std::mutex frame_mu;          // one pp_plan_frame at a time per device (frame scratch + car table)
     void* stage = nullptr;        // pp_plan_batch_host staging buffer
     size_t stage_cap = 0;
     std::mutex stage_mu;          // one pp_plan_batch_host at a time per device
-    bool table_reset = true;      // pp_plan_frame's persistent car table must be cleared
-    struct PlanTab {              // pp_plan_frame's car table (host copy between frames)
-        double s[PP_MAX_CARS], d[PP_MAX_CARS], vs[PP_MAX_CARS], vd[PP_MAX_CARS], vx[PP_MAX_CARS], vy[PP_MAX_CARS];
-        int32_t valid[PP_MAX_CARS], lane[PP_MAX_CARS];
-    } plan_tab;
+    pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
     bool timing = false;          // pp_timing_enable
     std::vector<hipEvent_t> ev_pool;
     std::vector<hipEvent_t> ev_rec; // groups of 4: before k_prep, after k_prep, after k_cand, after k_winner
@@ -1955,32 +2005,64 @@ PrepV prep_bind(void* base, int64_t S) {
     return p;
 }
 
-int ensure_ws(pp_map* M, int device, int64_t Sv) {
-    DevState& D = M->dev[device];
-    if (D.ws_cap >= Sv) return PP_OK;
-    if (D.ws) { (void)hipDeviceSynchronize(); (void)hipFree(D.ws); D.ws = nullptr; D.ws_cap = 0; }
-    if (hipMalloc(&D.ws, prep_bytes(Sv)) != hipSuccess) return PP_ERR_NOMEM;
-    D.ws_cap = Sv;
-    return PP_OK;
-}
-
-int ensure_rec(pp_map* M, int device, int64_t S) {
-    DevState& D = M->dev[device];
-    if (D.rec_cap >= S) return PP_OK;
-    if (D.rec) { (void)hipDeviceSynchronize(); (void)hipFree(D.rec); D.rec = nullptr; D.rec_cap = 0; }
-    if (hipMalloc(&D.rec, rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
-    D.rec_cap = S;
-    return PP_OK;
-}
-
-int n_draws(const pp_params* p) { return p->n_draws > 1 ? p->n_draws : 1; }
-
 int cands_per_block(int C) {
     int spb = 256 / C;
     if (spb > 64 / NL) spb = 64 / NL;      // <= 64 LDS spline slots per workgroup
     if (spb < 1) spb = 1;
     return spb;
 }
+
+// callers hold M->mu; `st` is the stream the workspace belongs to
+int ensure_ws(StreamWS& W, hipStream_t st, int64_t Sv) {
+    if (W.ws_cap >= Sv) return PP_OK;
+    if (W.ws) { (void)hipStreamSynchronize(st); (void)hipFree(W.ws); W.ws = nullptr; W.ws_cap = 0; }
+    if (hipMalloc(&W.ws, prep_bytes(Sv)) != hipSuccess) return PP_ERR_NOMEM;
+    W.ws_cap = Sv;
+    return PP_OK;
+}
+
+int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
+    if (W.rec_cap >= S) return PP_OK;
+    if (W.rec) { (void)hipStreamSynchronize(st); (void)hipFree(W.rec); W.rec = nullptr; W.rec_cap = 0; }
+    if (hipMalloc(&W.rec, rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
+    W.rec_cap = S;
+    return PP_OK;
+}
+
+int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
+    const int64_t words = (ngroups + 31) / 32;
+    if (W.gbits_cap >= words) return PP_OK;
+    if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
+    const int64_t cap = std::max<int64_t>(words, 1024);
+    if (hipMalloc(&W.gbits, sizeof(uint32_t) * cap) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMemsetAsync(W.gbits, 0, sizeof(uint32_t) * cap, st) != hipSuccess) return PP_ERR_HIP;
+    W.gbits_cap = cap;
+    return PP_OK;
+}
+
+void free_ws(StreamWS& W) {
+    if (W.ws) (void)hipFree(W.ws);
+    if (W.rec) (void)hipFree(W.rec);
+    if (W.gbits) (void)hipFree(W.gbits);
+    W = StreamWS();
+}
+
+// k_cand's launch geometry for C candidates per scene (BPS == 1: SPB scenes per group; else one
+// scene over BPS groups of 256 candidates)
+struct CandGeom { int spb, bps, threads; size_t lds; int64_t groups; };
+CandGeom cand_geom(int C, int64_t S) {
+    CandGeom g;
+    g.spb = C <= 256 ? cands_per_block(C) : 1;
+    g.bps = C <= 256 ? 1 : (C + 255) / 256;
+    g.threads = C <= 256 ? ((g.spb * C + 63) / 64) * 64 : 256;
+    const int nslot = NL * g.spb;
+    g.lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * g.spb;
+    g.groups = g.bps == 1 ? (S + g.spb - 1) / g.spb : S * g.bps;
+    return g;
+}
+
+int n_draws(const pp_params* p) { return p->n_draws > 1 ? p->n_draws : 1; }
+
 
 bool params_ok(const pp_params* p) {
     return p && p->n_points > PP_PREV_KEEP && p->n_points <= PP_MAX_POINTS && p->n_speeds >= 1 &&
@@ -2127,8 +2209,8 @@ int32_t pp_map_destroy(pp_map* M) {
         DeviceGuard g(d);
         (void)hipDeviceSynchronize();
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
-        if (D.ws) (void)hipFree(D.ws);
-        if (D.rec) (void)hipFree(D.rec);
+        for (auto& kv : D.sws) free_ws(kv.second);
+        D.sws.clear();
         if (D.frame) (void)hipFree(D.frame);
         if (D.stage) (void)hipFree(D.stage);
         for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
@@ -2150,9 +2232,10 @@ int32_t pp_reserve(pp_map* M, int32_t device, int64_t max_scenes) {
     DeviceGuard g(device);
     int rc = dev_init(M, device);
     if (rc) return rc;
-    rc = ensure_ws(M, device, max_scenes);
+    StreamWS& W = M->dev[device].sws[nullptr];       // the null stream's workspace
+    rc = ensure_ws(W, nullptr, max_scenes);
     if (rc) return rc;
-    return ensure_rec(M, device, max_scenes);
+    return ensure_rec(W, nullptr, max_scenes);
 }
 
 int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
@@ -2168,7 +2251,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         return PP_ERR_ARG;
     if (prm->emit_paths && !out->paths) return PP_ERR_ARG;
     if (in->tab_valid && (!in->tab_lane || !in->tab_s || !in->tab_d || !in->tab_vs || !in->tab_vd ||
-                          !in->tab_vx || !in->tab_vy || prm->n_draws > 1))
+                          !in->tab_vx || !in->tab_vy || prm->n_draws > 1 || in->tab_slots < 0 ||
+                          in->tab_slots > PP_MAX_CARS))
         return PP_ERR_ARG;
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)hip_stream;
@@ -2178,51 +2262,53 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     // reference decision without draws: the winner is known before the loop (k_cand records it,
     // k_emit writes it); otherwise the decision is a cost argmin (k_winner)
     const bool ref_direct = prm->cost_mode == PP_COST_REFERENCE && Dn == 1;
-    PrepV pv;
-    MapG mg;
+    const CandGeom cg = cand_geom(Dn * NL * prm->n_speeds, S);
+    if (cg.groups > 0x7fffffff) return PP_ERR_ARG;
+    // the map lock is held from workspace binding through the (asynchronous) launches: a
+    // concurrent call cannot grow and free this stream's buffers in between
+    std::lock_guard<std::mutex> lk(M->mu);
+    int rc = dev_init(M, device);
+    if (rc) return rc;
+    DevState& DS = M->dev[device];
+    StreamWS& W = DS.sws[hip_stream];
+    rc = ensure_ws(W, st, Sv);
+    if (rc) return rc;
+    rc = ensure_gbits(W, st, cg.groups);
+    if (rc) return rc;
     double* rec = nullptr;
     uint64_t* adjm = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(M->mu);
-        int rc = dev_init(M, device);
+    if (ref_direct && !prm->emit_paths) {
+        rc = ensure_rec(W, st, S);
         if (rc) return rc;
-        rc = ensure_ws(M, device, Sv);
-        if (rc) return rc;
-        if (ref_direct && !prm->emit_paths) {
-            rc = ensure_rec(M, device, S);
-            if (rc) return rc;
-            rec = rec_buf(M->dev[device].rec);
-            adjm = adj_buf(M->dev[device].rec, M->dev[device].rec_cap);
-        }
-        pv = prep_bind(M->dev[device].ws, M->dev[device].ws_cap);
-        mg.buf = M->dev[device].map;
-        mg.n = M->n;
-        mg.fastm = M->fastm;
+        rec = rec_buf(W.rec);
+        adjm = adj_buf(W.rec, W.rec_cap);
     }
+    const PrepV pv = prep_bind(W.ws, W.ws_cap);
+    MapG mg;
+    mg.buf = DS.map;
+    mg.n = M->n;
+    mg.fastm = M->fastm;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    bool timing = false;
-    {
-        std::lock_guard<std::mutex> lk(M->mu);
-        DevState& D = M->dev[device];
-        if (D.timing) {
-            timing = true;
-            for (int i = 0; i < 4; i++) {
-                if (D.ev_pool.empty()) {
-                    hipEvent_t e;
-                    if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
-                    D.ev_pool.push_back(e);
-                }
-                ev[i] = D.ev_pool.back();
-                D.ev_pool.pop_back();
-                D.ev_rec.push_back(ev[i]);
+    const bool timing = DS.timing;
+    if (timing) {
+        for (int i = 0; i < 4; i++) {
+            if (DS.ev_pool.empty()) {
+                hipEvent_t e;
+                if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
+                DS.ev_pool.push_back(e);
             }
-            D.ev_has3.push_back(!(ref_direct && prm->emit_paths) ? 1 : 0);
+            ev[i] = DS.ev_pool.back();
+            DS.ev_pool.pop_back();
+            DS.ev_rec.push_back(ev[i]);
         }
+        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) ? 1 : 0);
     }
     pp_params P = *prm;
     pp_scene_batch B = *in;
     pp_result R = *out;
     if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
+    GroupBits gb;
+    gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     // K1
     {
         const int threads = 256;
@@ -2230,34 +2316,26 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (timing) (void)hipEventRecord(ev[0], st);
         if (mg.n <= kLdsMapMax) {
             const size_t lds = sizeof(double) * kMapArrays * (size_t)mg.n;
-            hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status);
+            hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb);
         } else {
-            hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status);
+            hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb);
         }
     }
-    // K2
+    // K2: the full grid for the scenes in the proven range, then the flagged groups only
     {
-        // a block holds SPB whole scenes (all draws: the spline slots are shared by the draws),
-        // or, when a scene has more than 256 candidates, BPS blocks share one scene
-        const int C = Dn * NL * P.n_speeds;
-        const int spb = C <= 256 ? cands_per_block(C) : 1;
-        const int bps = C <= 256 ? 1 : (C + 255) / 256;
-        const int threads = C <= 256 ? ((spb * C + 63) / 64) * 64 : 256;
-        const int nslot = NL * spb;
-        const size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * spb;
-        const int64_t blocks = bps == 1 ? (S + spb - 1) / spb : S * bps;
-        if (blocks > 0x7fffffff) return PP_ERR_ARG;
+        const unsigned nb = (unsigned)cg.groups;
+        const unsigned nslow = (unsigned)std::min<int64_t>(cg.groups, 2048);
+        const int64_t ng = cg.groups;
         if (timing) (void)hipEventRecord(ev[1], st);
-        if (P.emit_paths) {
-            hipLaunchKernelGGL((k_cand<false, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 2>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-        } else if (ref_direct) {
-            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-        } else {
-            hipLaunchKernelGGL((k_cand<false, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-            hipLaunchKernelGGL((k_cand<true, 0>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R, spb, bps, rec, adjm);
-        }
+#define PP_LAUNCH_CAND(MODE)                                                                              \
+        hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng);                                         \
+        hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng)
+        if (P.emit_paths) { PP_LAUNCH_CAND(2); }
+        else if (ref_direct) { PP_LAUNCH_CAND(1); }
+        else { PP_LAUNCH_CAND(0); }
+#undef PP_LAUNCH_CAND
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
@@ -2339,7 +2417,8 @@ int32_t pp_synth_scenes_host(const pp_map* M, uint64_t seed, int64_t first_scene
 int32_t pp_synth_traffic(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* tel,
                          pp_traffic* out, int32_t device, void* hip_stream) {
     if (!M || !tel || device < 0 || device >= kMaxDev || tel->n_scenes < 0 || first_scene < 0 ||
-        tel->car_stride < ppsynth::kSynthCars || !traffic_ok(out, tel))
+        tel->car_stride < ppsynth::kSynthCars || !traffic_ok(out, tel) ||
+        (tel->tab_valid && (tel->tab_slots < ppsynth::kSynthCars || tel->tab_slots > PP_MAX_CARS)))
         return PP_ERR_ARG;
     if (tel->n_scenes == 0) return PP_OK;
     DeviceGuard g(device);
@@ -2362,7 +2441,8 @@ int32_t pp_synth_traffic(pp_map* M, uint64_t seed, int64_t first_scene, pp_scene
 int32_t pp_synth_traffic_host(const pp_map* M, uint64_t seed, int64_t first_scene, pp_scene_batch* tel,
                               pp_traffic* out) {
     if (!M || !tel || tel->n_scenes < 0 || first_scene < 0 || tel->car_stride < ppsynth::kSynthCars ||
-        !traffic_ok(out, tel))
+        !traffic_ok(out, tel) ||
+        (tel->tab_valid && (tel->tab_slots < ppsynth::kSynthCars || tel->tab_slots > PP_MAX_CARS)))
         return PP_ERR_ARG;
     const ppsynth::LaneTables T = lane_tables(M->lanetab.data(), M->n);
     out->n_cars = ppsynth::kSynthCars;
@@ -2370,8 +2450,10 @@ int32_t pp_synth_traffic_host(const pp_map* M, uint64_t seed, int64_t first_scen
     const ppsynth::TrafficV tv = traffic_view(out, o.S);
     for (int64_t s = 0; s < o.S; s++) {
         ppsynth::synth_scene(T, seed, first_scene + s, s, o, &tv);
-        if (tel->tab_valid)
-            for (int j = 0; j < PP_MAX_CARS; j++) tel->tab_valid[(int64_t)j * o.S + s] = 0;
+        for (int j = 0; tel->tab_valid && j < tel->tab_slots; j++) {
+            tel->tab_valid[(int64_t)j * o.S + s] = 0;
+            if (tel->tab_id) tel->tab_id[(int64_t)j * o.S + s] = j;
+        }
     }
     return PP_OK;
 }
@@ -2383,7 +2465,8 @@ int32_t pp_rollout(pp_map* M, pp_scene_batch* tel, pp_traffic* traffic, const pp
         return PP_ERR_ARG;
     if (cfg->n_frames < 0 || cfg->consume < 1 || !(cfg->sensor_range >= 0) || prm->n_draws > 1 ||
         prm->emit_paths || !tel->tab_valid || !tel->tab_lane || !tel->tab_s || !tel->tab_d ||
-        !tel->tab_vs || !tel->tab_vd || !tel->tab_vx || !tel->tab_vy || tel->car_stride < traffic->n_cars)
+        !tel->tab_vs || !tel->tab_vd || !tel->tab_vx || !tel->tab_vy || tel->car_stride < traffic->n_cars ||
+        tel->tab_slots < traffic->n_cars)
         return PP_ERR_ARG;
     if (log && log->plan_x && !log->plan_y) return PP_ERR_ARG;
     if (tel->n_scenes == 0 || cfg->n_frames == 0) return PP_OK;
@@ -2427,8 +2510,10 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     const int C = n_draws(prm) * NL * prm->n_speeds;
     const bool tab = hin->tab_valid != nullptr;
     // staging layout: doubles first, then 4-byte fields
-    const size_t nd = (size_t)S * (4 + 2 * PP_PREV_KEEP + 4 * J + (tab ? 6 * PP_MAX_CARS : 0) + 2 * N + C);
-    const size_t ni = (size_t)S * (3 + J + (tab ? 2 * PP_MAX_CARS : 0) + 3);
+    const int TS = tab ? hin->tab_slots : 0;
+    if (tab && (TS < 0 || TS > PP_MAX_CARS)) return PP_ERR_ARG;
+    const size_t nd = (size_t)S * (4 + 2 * PP_PREV_KEEP + 4 * J + 6 * TS + 2 * N + C);
+    const size_t ni = (size_t)S * (3 + J + 3 * TS + 3);
     const size_t bytes = nd * 8 + ni * 4 + 256;
     DeviceGuard g(device);
     hipStream_t st = (hipStream_t)hip_stream;
@@ -2472,10 +2557,11 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     }
     double* tabd = nullptr;
     if (tab) {
-        tabd = takeD(6 * PP_MAX_CARS * S);
+        tabd = takeD(6 * (size_t)TS * S);
         const double* src[6] = {hin->tab_s, hin->tab_d, hin->tab_vs, hin->tab_vd, hin->tab_vx, hin->tab_vy};
         double** dst[6] = {&B.tab_s, &B.tab_d, &B.tab_vs, &B.tab_vd, &B.tab_vx, &B.tab_vy};
-        for (int k = 0; k < 6; k++) { *dst[k] = tabd + k * PP_MAX_CARS * S; h2d(*dst[k], src[k], 8 * PP_MAX_CARS * S); }
+        for (int k = 0; k < 6; k++) { *dst[k] = tabd + k * (size_t)TS * S; h2d(*dst[k], src[k], 8 * (size_t)TS * S); }
+        B.tab_slots = TS;
     }
     double* nxy = takeD(2 * (size_t)N * S);
     double* cost = takeD((size_t)C * S);
@@ -2487,9 +2573,10 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     h2d(cid, hin->car_id, 4 * J * S);
     int32_t* tabi = nullptr;
     if (tab) {
-        tabi = takeI(2 * PP_MAX_CARS * S);
-        B.tab_valid = tabi; B.tab_lane = tabi + PP_MAX_CARS * S;
-        h2d(tabi, hin->tab_valid, 4 * PP_MAX_CARS * S); h2d(tabi + PP_MAX_CARS * S, hin->tab_lane, 4 * PP_MAX_CARS * S);
+        tabi = takeI(3 * (size_t)TS * S);
+        B.tab_valid = tabi; B.tab_lane = tabi + (size_t)TS * S;
+        h2d(tabi, hin->tab_valid, 4 * (size_t)TS * S); h2d(tabi + (size_t)TS * S, hin->tab_lane, 4 * (size_t)TS * S);
+        if (hin->tab_id) { B.tab_id = tabi + 2 * (size_t)TS * S; h2d(B.tab_id, hin->tab_id, 4 * (size_t)TS * S); }
     }
     int32_t* outi = takeI(3 * S);
     pp_result R;
@@ -2507,8 +2594,8 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     d2h(hout->cost, R.cost, 8 * (size_t)C * S);
     if (tab) {
         double* dstd[6] = {hin->tab_s, hin->tab_d, hin->tab_vs, hin->tab_vd, hin->tab_vx, hin->tab_vy};
-        for (int k = 0; k < 6; k++) d2h(dstd[k], tabd + k * PP_MAX_CARS * S, 8 * PP_MAX_CARS * S);
-        d2h(hin->tab_valid, tabi, 4 * PP_MAX_CARS * S); d2h(hin->tab_lane, tabi + PP_MAX_CARS * S, 4 * PP_MAX_CARS * S);
+        for (int k = 0; k < 6; k++) d2h(dstd[k], tabd + k * (size_t)TS * S, 8 * (size_t)TS * S);
+        d2h(hin->tab_valid, tabi, 4 * (size_t)TS * S); d2h(hin->tab_lane, tabi + (size_t)TS * S, 4 * (size_t)TS * S);
     }
     if (!ok || hipStreamSynchronize(st) != hipSuccess) return PP_ERR_HIP;
     return PP_OK;
@@ -2516,8 +2603,8 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
 
 int32_t pp_plan_reset(pp_map* M, int32_t device) {
     if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
-    std::lock_guard<std::mutex> lk(M->mu);
-    M->dev[device].table_reset = true;
+    std::lock_guard<std::mutex> lk(M->dev[device].frame_mu);
+    M->dev[device].plan_table.cars.clear();
     return PP_OK;
 }
 
@@ -2545,17 +2632,16 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     const int nc = (int)rows.size();
     // device scratch layout (bytes): doubles then ints
     constexpr int N = 50;
+    constexpr int TS = PP_MAX_CARS;
     struct Frame {
         double ego[4], px[PP_PREV_KEEP], py[PP_PREV_KEEP], cx[PP_MAX_CARS], cy[PP_MAX_CARS],
             cvx[PP_MAX_CARS], cvy[PP_MAX_CARS];
         double nx[N], ny[N], cost[NL];
-        DevState::PlanTab tab;
+        double ts[TS], td[TS], tvs[TS], tvd[TS], tvx[TS], tvy[TS];        // the car table's slots
+        int32_t tid[TS], tvalid[TS], tlane[TS];
         int32_t nprev, ptl, ncars, cid[PP_MAX_CARS], winner, nout;
         uint32_t status;
     };
-    // the reference's car table persists across frames when every id fits a slot
-    bool use_tab = true;
-    for (const Row& r : rows) if (r.id < 0 || r.id >= PP_MAX_CARS) use_tab = false;
     Frame h;
     memset(&h, 0, sizeof(h));
     h.ego[0] = ego_x; h.ego[1] = ego_y; h.ego[2] = ego_yaw_deg; h.ego[3] = ego_speed_mph;
@@ -2565,16 +2651,19 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         h.cid[j] = rows[j].id; h.cx[j] = rows[j].x; h.cy[j] = rows[j].y; h.cvx[j] = rows[j].vx; h.cvy[j] = rows[j].vy;
     }
     DeviceGuard g(device);
+    std::lock_guard<std::mutex> frame_lock(M->dev[device].frame_mu);
+    DevState& DS = M->dev[device];
+    // the reference's std::map, laid out over the union of its ids and this frame's (any ints)
+    const pptab::Slots hs = {1, h.tid, h.tvalid, h.tlane, h.ts, h.td, h.tvs, h.tvd, h.tvx, h.tvy};
+    const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS);
+    if (nslots < 0) return PP_ERR_ARG;                  // more than PP_MAX_CARS distinct cars
     Frame* d = nullptr;
     {
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
         if (rc) return rc;
-        if (!M->dev[device].frame && hipMalloc(&M->dev[device].frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
-        d = (Frame*)M->dev[device].frame;
-        DevState& D = M->dev[device];
-        if (D.table_reset) { memset(&D.plan_tab, 0, sizeof(D.plan_tab)); D.table_reset = false; }
-        h.tab = D.plan_tab;
+        if (!DS.frame && hipMalloc(&DS.frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
+        d = (Frame*)DS.frame;
     }
     if (hipMemcpy(d, &h, sizeof(Frame), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
     pp_scene_batch B;
@@ -2583,10 +2672,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     B.ego_x = &d->ego[0]; B.ego_y = &d->ego[1]; B.ego_yaw_deg = &d->ego[2]; B.ego_speed_mph = &d->ego[3];
     B.prev_x = d->px; B.prev_y = d->py; B.n_prev = &d->nprev; B.prev_target_lane = &d->ptl;
     B.n_cars = &d->ncars; B.car_id = d->cid; B.car_x = d->cx; B.car_y = d->cy; B.car_vx = d->cvx; B.car_vy = d->cvy;
-    if (use_tab) {
-        B.tab_valid = d->tab.valid; B.tab_lane = d->tab.lane; B.tab_s = d->tab.s; B.tab_d = d->tab.d;
-        B.tab_vs = d->tab.vs; B.tab_vd = d->tab.vd; B.tab_vx = d->tab.vx; B.tab_vy = d->tab.vy;
-    }
+    B.tab_slots = nslots; B.tab_id = d->tid;
+    B.tab_valid = d->tvalid; B.tab_lane = d->tlane; B.tab_s = d->ts; B.tab_d = d->td;
+    B.tab_vs = d->tvs; B.tab_vd = d->tvd; B.tab_vx = d->tvx; B.tab_vy = d->tvy;
     pp_params P;
     pp_params_default(&P);
     P.n_speeds = 1;
@@ -2603,10 +2691,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     if (rc == PP_OK && hipMemcpy(&hi, dinfo, sizeof(hi), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
     (void)hipFree(dinfo);
     if (rc != PP_OK) return rc;
-    if (use_tab) {
-        std::lock_guard<std::mutex> lk(M->mu);
-        M->dev[device].plan_tab = h.tab;
-    }
+    DS.plan_table.take_back(hs, 0, nslots);
     *n_out = h.nout;
     for (int i = 0; i < h.nout && i < N; i++) { next_x[i] = h.nx[i]; next_y[i] = h.ny[i]; }
     *target_lane = hi.target_lane;

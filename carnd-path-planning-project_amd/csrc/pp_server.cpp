@@ -21,6 +21,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <deque>
 #include <memory>
@@ -28,6 +29,7 @@
 #include <vector>
 
 #include "../../include/pp.h"
+#include "pp_cartable.h"
 
 namespace {
 
@@ -100,9 +102,7 @@ struct Conn {
     std::deque<std::string> msgs;   // complete text messages, in order
     // the reference lambda's captures (src/main.cpp:1194-1195)
     int32_t target_lane = 1;
-    int32_t tvalid[PP_MAX_CARS] = {0}, tlane[PP_MAX_CARS] = {0};
-    double ts[PP_MAX_CARS] = {0}, td[PP_MAX_CARS] = {0}, tvs[PP_MAX_CARS] = {0}, tvd[PP_MAX_CARS] = {0},
-           tvx[PP_MAX_CARS] = {0}, tvy[PP_MAX_CARS] = {0};
+    pptab::CarTable table;          // std::map<int, Car> sensor_fusion_cars (any ids)
 };
 
 // HTTP upgrade; false = not complete yet; sets c.closing on a bad request
@@ -209,7 +209,7 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
     const int J = PP_MAX_CARS, N = prm.n_points, C = PP_NUM_LANES * prm.n_speeds;
     // host batch (SoA, cap scenes) + results
     std::vector<double> ego(4 * cap), pxy(2 * PP_PREV_KEEP * cap), cars(4 * J * cap), tabd(6 * PP_MAX_CARS * cap);
-    std::vector<int32_t> ints(3 * cap), cid(J * cap), tabi(2 * PP_MAX_CARS * cap), mst(cap);
+    std::vector<int32_t> ints(3 * cap), cid(J * cap), tabi(3 * PP_MAX_CARS * cap), mst(cap);
     std::vector<double> nxy(2 * N * cap), cost(C * cap);
     std::vector<int32_t> win(cap), nout(cap);
     std::vector<uint32_t> status(cap);
@@ -276,8 +276,26 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
             rc = pp_telemetry_parse(buf.data(), off.data(), A, &B, mst.data(), o->threads);
             if (rc != PP_OK) break;
             // dense batch of the telemetry frames, with each connection's state
+            // status 2 (more distinct cars than PP_MAX_CARS) is not planned: the reference would
+            // use every car, the batch holds PP_MAX_CARS; such a connection is closed
             std::vector<int> tel;
-            for (int i = 0; i < A; i++) if (mst[i] == 0 || mst[i] == 2) tel.push_back(i);
+            for (int i = 0; i < A; i++) {
+                if (mst[i] == 0) tel.push_back(i);
+                else if (mst[i] == 2) conns[who[i]]->closing = true;
+            }
+            // a frame whose car table would exceed PP_MAX_CARS distinct cars: closed the same way
+            {
+                std::vector<int> keep;
+                for (int i : tel) {
+                    Conn& c = *conns[who[i]];
+                    const int nc = ((const int32_t*)B.n_cars)[i];
+                    std::vector<int32_t> ids(nc);
+                    for (int j = 0; j < nc; j++) ids[j] = B.car_id[(size_t)j * A + i];
+                    if (c.table.union_size(ids.data(), nc) > PP_MAX_CARS) c.closing = true;
+                    else keep.push_back(i);
+                }
+                tel.swap(keep);
+            }
             const int T = (int)tel.size();
             if (T) {
                 // compact in place (tel is increasing, so i <= tel[i])
@@ -295,18 +313,32 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
                 D.prev_x = pxy.data(); D.prev_y = pxy.data() + PP_PREV_KEEP * T;
                 D.n_prev = ints.data(); D.prev_target_lane = ints.data() + T; D.n_cars = ints.data() + 2 * T;
                 D.car_x = cars.data(); D.car_y = cars.data() + J * T; D.car_vx = cars.data() + 2 * J * T; D.car_vy = cars.data() + 3 * J * T;
-                D.tab_valid = tabi.data(); D.tab_lane = tabi.data() + PP_MAX_CARS * T;
-                D.tab_s = tabd.data(); D.tab_d = tabd.data() + PP_MAX_CARS * T; D.tab_vs = tabd.data() + 2 * PP_MAX_CARS * T;
-                D.tab_vd = tabd.data() + 3 * PP_MAX_CARS * T; D.tab_vx = tabd.data() + 4 * PP_MAX_CARS * T;
-                D.tab_vy = tabd.data() + 5 * PP_MAX_CARS * T;
+                // each connection's car table laid out over the union of its ids and its frame's
+                // ids (pp_cartable.h), padded to the batch's largest union
+                int TSl = 0;
+                std::vector<int> used(T);
+                for (int i = 0; i < T; i++) {
+                    const int nc = D.n_cars[i];
+                    std::vector<int32_t> ids(nc);
+                    for (int j = 0; j < nc; j++) ids[j] = D.car_id[(size_t)j * T + i];
+                    used[i] = conns[who[tel[i]]]->table.union_size(ids.data(), nc);
+                    TSl = std::max(TSl, used[i]);
+                }
+                D.tab_slots = TSl;
+                D.tab_id = tabi.data() + 2 * (size_t)TSl * T;
+                D.tab_valid = tabi.data(); D.tab_lane = tabi.data() + (size_t)TSl * T;
+                D.tab_s = tabd.data(); D.tab_d = tabd.data() + (size_t)TSl * T; D.tab_vs = tabd.data() + 2 * (size_t)TSl * T;
+                D.tab_vd = tabd.data() + 3 * (size_t)TSl * T; D.tab_vx = tabd.data() + 4 * (size_t)TSl * T;
+                D.tab_vy = tabd.data() + 5 * (size_t)TSl * T;
+                const pptab::Slots sl = {T, D.tab_id, D.tab_valid, D.tab_lane, D.tab_s, D.tab_d, D.tab_vs, D.tab_vd,
+                                         D.tab_vx, D.tab_vy};
                 for (int i = 0; i < T; i++) {
                     Conn& c = *conns[who[tel[i]]];
                     ((int32_t*)D.prev_target_lane)[i] = c.target_lane;
-                    for (int j = 0; j < PP_MAX_CARS; j++) {
-                        const size_t x = (size_t)j * T + i;
-                        D.tab_valid[x] = c.tvalid[j]; D.tab_lane[x] = c.tlane[j]; D.tab_s[x] = c.ts[j]; D.tab_d[x] = c.td[j];
-                        D.tab_vs[x] = c.tvs[j]; D.tab_vd[x] = c.tvd[j]; D.tab_vx[x] = c.tvx[j]; D.tab_vy[x] = c.tvy[j];
-                    }
+                    const int nc = D.n_cars[i];
+                    std::vector<int32_t> ids(nc);
+                    for (int j = 0; j < nc; j++) ids[j] = D.car_id[(size_t)j * T + i];
+                    c.table.layout(ids.data(), nc, sl, i, TSl);
                 }
                 pp_result R;
                 memset(&R, 0, sizeof(R));
@@ -317,11 +349,7 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
                 for (int i = 0; i < T; i++) {
                     Conn& c = *conns[who[tel[i]]];
                     c.target_lane = win[i] / prm.n_speeds;
-                    for (int j = 0; j < PP_MAX_CARS; j++) {
-                        const size_t x = (size_t)j * T + i;
-                        c.tvalid[j] = D.tab_valid[x]; c.tlane[j] = D.tab_lane[x]; c.ts[j] = D.tab_s[x]; c.td[j] = D.tab_d[x];
-                        c.tvs[j] = D.tab_vs[x]; c.tvd[j] = D.tab_vd[x]; c.tvx[j] = D.tab_vx[x]; c.tvy[j] = D.tab_vy[x];
-                    }
+                    c.table.take_back(sl, i, used[i]);
                 }
                 int64_t need = 0;
                 ooff.assign(T + 1, 0);

@@ -36,7 +36,7 @@ def _open():
 _LIB = _open()
 NUM_LANES = int(_LIB.pp_num_lanes())   # PP_NUM_LANES the library was built for (src/main.cpp:22)
 PREV_KEEP = 10
-MAX_CARS = 16
+MAX_CARS = 64            # PP_MAX_CARS: sensor_fusion rows and car-table slots per scene
 MAX_SPEEDS = 8
 MAX_POINTS = 128
 
@@ -56,17 +56,17 @@ _up = C.POINTER(C.c_uint32)
 
 
 class SceneBatch(C.Structure):
-    _fields_ = [("n_scenes", C.c_int64), ("car_stride", C.c_int32), ("_pad", C.c_int32),
+    _fields_ = [("n_scenes", C.c_int64), ("car_stride", C.c_int32), ("tab_slots", C.c_int32),
                 ("ego_x", C.c_void_p), ("ego_y", C.c_void_p), ("ego_yaw_deg", C.c_void_p),
                 ("ego_speed_mph", C.c_void_p), ("prev_x", C.c_void_p), ("prev_y", C.c_void_p),
                 ("n_prev", C.c_void_p), ("prev_target_lane", C.c_void_p), ("n_cars", C.c_void_p),
                 ("car_id", C.c_void_p), ("car_x", C.c_void_p), ("car_y", C.c_void_p),
                 ("car_vx", C.c_void_p), ("car_vy", C.c_void_p),
-                ("tab_valid", C.c_void_p), ("tab_lane", C.c_void_p), ("tab_s", C.c_void_p),
+                ("tab_id", C.c_void_p), ("tab_valid", C.c_void_p), ("tab_lane", C.c_void_p), ("tab_s", C.c_void_p),
                 ("tab_d", C.c_void_p), ("tab_vs", C.c_void_p), ("tab_vd", C.c_void_p),
                 ("tab_vx", C.c_void_p), ("tab_vy", C.c_void_p)]
 
-TABLE_FIELDS_I = ["tab_valid", "tab_lane"]
+TABLE_FIELDS_I = ["tab_id", "tab_valid", "tab_lane"]
 TABLE_FIELDS_F = ["tab_s", "tab_d", "tab_vs", "tab_vd", "tab_vx", "tab_vy"]
 
 
@@ -337,6 +337,8 @@ def scene_struct(d) -> SceneBatch:
         setattr(b, k, _ptr(d[k]))
     for k in TABLE_FIELDS_I + TABLE_FIELDS_F:
         setattr(b, k, _ptr(d.get(k)))
+    if d.get("tab_valid") is not None:
+        b.tab_slots = int(d["tab_valid"].shape[0])
     return b
 
 
@@ -348,21 +350,24 @@ def _mk(xp, device):
             lambda sh: torch.zeros(sh, dtype=torch.int32, device=device))
 
 
-def add_car_table(d, xp="numpy", device=None):
-    """Adds the persistent car table (include/pp.h tab_*; empty) to a scene dict."""
+def add_car_table(d, slots=12, xp="numpy", device=None):
+    """Adds the persistent car table (include/pp.h tab_*: `slots` slots per scene, slot j = id j,
+    empty) to a scene dict."""
     S = int(d["ego_x"].shape[0])
     zf, zi = _mk(xp, device)
     for k in TABLE_FIELDS_I:
-        d[k] = zi((MAX_CARS, S))
+        d[k] = zi((slots, S))
     for k in TABLE_FIELDS_F:
-        d[k] = zf((MAX_CARS, S))
+        d[k] = zf((slots, S))
+    for j in range(slots):
+        d["tab_id"][j] = j
     return d
 
 
-def alloc_traffic(S, xp="numpy", device=None):
+def alloc_traffic(S, n=12, xp="numpy", device=None):
     zf, zi = _mk(xp, device)
-    return {"n_cars": 0, "lane": zi((MAX_CARS, S)), "seg": zi((MAX_CARS, S)), "t": zf((MAX_CARS, S)),
-            "offset": zf((MAX_CARS, S)), "speed": zf((MAX_CARS, S))}
+    return {"n_cars": 0, "lane": zi((n, S)), "seg": zi((n, S)), "t": zf((n, S)),
+            "offset": zf((n, S)), "speed": zf((n, S))}
 
 
 def traffic_struct(t) -> Traffic:

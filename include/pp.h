@@ -34,7 +34,7 @@ extern "C" {
 #define PP_NUM_LANES   3    /* library is built for one value: pp_num_lanes() reports it)      */
 #endif
 #define PP_PREV_KEEP   10   /* src/main.cpp:1258 prev_trajectory_length                       */
-#define PP_MAX_CARS    16   /* sensor_fusion rows per scene (simulator sends 12)              */
+#define PP_MAX_CARS    64   /* sensor_fusion rows per scene and car-table slots (simulator: 12) */
 #define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
 #define PP_MAX_POINTS  128  /* horizon N upper bound (reference: 50, src/main.cpp:854,1039)   */
 #define PP_MAX_KNOTS   16   /* spline knots: 9 prev + 1 + 5 control points (src/main.cpp:744) */
@@ -78,7 +78,7 @@ extern "C" {
 typedef struct pp_scene_batch {
     int64_t n_scenes;
     int32_t car_stride;            /* number of car columns (<= PP_MAX_CARS)                  */
-    int32_t _pad;
+    int32_t tab_slots;             /* car-table slots per scene (<= PP_MAX_CARS; see tab_*)    */
     const double*  ego_x;          /* telemetry x, src/main.cpp:1233                           */
     const double*  ego_y;          /* telemetry y                                              */
     const double*  ego_yaw_deg;    /* telemetry yaw (degrees)                                  */
@@ -95,10 +95,14 @@ typedef struct pp_scene_batch {
     const double*  car_vy;
     /* Optional persistent car table: the reference's cross-frame `std::map<int, Car>
      * sensor_fusion_cars` (src/main.cpp:1194, 1325-1350). NULL tab_valid = a fresh table every
-     * frame. Otherwise slot [id * n_scenes + s] (id < PP_MAX_CARS; the frame's car ids must be
-     * ascending and < PP_MAX_CARS) holds the car's last matched state: a reported car is
-     * re-matched and its slot overwritten, or erased (valid = 0) when matching fails (:1336-1340);
-     * a car absent from this frame's list keeps its stale slot, which the planner still uses. */
+     * frame. Otherwise the scene's table is tab_slots slots [k * n_scenes + s] in std::map order:
+     * slot k holds car id tab_id[k] (ascending over k; tab_id NULL: slot k is id k), and every car
+     * id of this frame's sensor_fusion rows is one of the slot ids (pp_plan_frame, pp_serve and the
+     * rollout lay the table out over the union of the stored ids and the frame's ids; any int
+     * ids). Visiting the slots in order, a reported car is re-matched and its slot overwritten, or
+     * erased (valid = 0) when matching fails (:1336-1340); an unreported valid slot is the car's
+     * stale entry, which the planner still uses; an invalid unreported slot is no car. */
+    int32_t* tab_id;
     int32_t* tab_valid;
     int32_t* tab_lane;
     double*  tab_s;
@@ -200,15 +204,19 @@ int32_t pp_map_geometry(const pp_map* m, double* out, int32_t n);
 int32_t pp_reserve(pp_map* m, int32_t device, int64_t max_scenes);
 
 /* Evaluate a batch. All batch/result pointers are device memory on `device`; `hip_stream` is a
- * hipStream_t (NULL = default stream). Asynchronous w.r.t. the host. */
+ * hipStream_t (NULL = default stream). Asynchronous w.r.t. the host. Thread-safe: every stream
+ * has its own device workspace, so calls on different streams may overlap; calls on one stream
+ * run in its order. */
 int32_t pp_eval(pp_map* m, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
                 int32_t device, void* hip_stream);
 
 /* One telemetry frame, host memory in/out: the onMessage replacement (C = 1, reference decision).
  * prev_x/prev_y hold n_prev points (only the first 10 are read when n_prev >= 10); the car arrays
- * hold n_cars rows in any order (sorted by id internally, as std::map does). The car table
- * persists across calls like the reference's (see pp_plan_reset) when every id is < PP_MAX_CARS.
- * *target_lane is read (cross-frame state) and updated. Writes up to 50 points. */
+ * hold n_cars rows (<= PP_MAX_CARS) in any order with any int ids (sorted by id internally, the
+ * last row of a repeated id wins, as std::map assignment does). The car table persists across
+ * calls like the reference's (see pp_plan_reset); PP_ERR_ARG if the table would hold more than
+ * PP_MAX_CARS distinct cars. *target_lane is read (cross-frame state) and updated. Writes up to
+ * 50 points. Calls on one map and device are serialised. */
 int32_t pp_plan_frame(pp_map* m, int32_t device,
                       double ego_x, double ego_y, double ego_yaw_deg, double ego_speed_mph,
                       const double* prev_x, const double* prev_y, int32_t n_prev,
@@ -232,7 +240,7 @@ int32_t pp_synth_scenes_host(const pp_map* m, uint64_t seed, int64_t first_scene
  * target lane (src/main.cpp:1195) to the plan's lane (winner / n_speeds), advances the traffic by
  * consume * 0.02 s and reports the cars within sensor_range (ascending id) as the next frame's
  * sensor_fusion; the others become stale car-table entries (tab_* above, required). */
-typedef struct pp_traffic {        /* device SoA [j * n_scenes + s]; car j has id j               */
+typedef struct pp_traffic {        /* device SoA [j * n_scenes + s]; car j has id j, table slot j  */
     int32_t  n_cars;               /* cars per scene (<= PP_MAX_CARS)                               */
     int32_t  _pad;
     int32_t* lane;                 /* lane-centre polyline it follows                              */
@@ -263,9 +271,10 @@ typedef struct pp_rollout_log {
     double*   plan_y;
 } pp_rollout_log;
 
-/* Runs cfg->n_frames frames; `telemetry` (with its car table), `traffic` and `result` (per-frame
- * plan buffers, pp_eval layout) are device state updated in place, so consecutive calls continue
- * the episode. n_draws must be <= 1 and emit_paths 0. */
+/* Runs cfg->n_frames frames; `telemetry` (with its car table: tab_slots >= traffic n_cars, slot j
+ * = car j, tab_id NULL or j), `traffic` and `result` (per-frame plan buffers, pp_eval layout) are
+ * device state updated in place, so consecutive calls continue the episode. n_draws must be <= 1
+ * and emit_paths 0. */
 int32_t pp_rollout(pp_map* m, pp_scene_batch* telemetry, pp_traffic* traffic,
                    const pp_params* prm, const pp_rollout_cfg* cfg, pp_result* result,
                    pp_rollout_log* log, int32_t device, void* hip_stream);
@@ -286,8 +295,8 @@ int32_t pp_synth_traffic_host(const pp_map* m, uint64_t seed, int64_t first_scen
 int32_t pp_plan_batch_host(pp_map* m, int32_t device, pp_scene_batch* host_in, const pp_params* prm,
                            pp_result* host_out, void* hip_stream);
 
-/* pp_plan_frame keeps the reference's car table across calls (per map and device, cars with ids
- * in [0, PP_MAX_CARS)); pp_plan_reset empties it (a new episode). */
+/* pp_plan_frame keeps the reference's car table across calls (per map and device, any ids);
+ * pp_plan_reset empties it (a new episode). */
 int32_t pp_plan_reset(pp_map* m, int32_t device);
 
 /* ---- simulator wire codec (host code) ----------------------------- */

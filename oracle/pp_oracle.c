@@ -516,11 +516,11 @@ typedef struct {
 static const uint32_t limit_flag[5] = {0, PP_ST_BRAKE, PP_ST_MAXBRAKE, PP_ST_ADJUST, PP_ST_KEEP};
 
 /* Monte-Carlo sensor noise (build extension, include/pp.h pp_params / pp_mc_gauss): Philox4x32-10
- * block keyed by the seed, counter {scene, (draw * 16 + car) * 4 + q, 0x4D43}; Irwin-Hall of its
+ * block keyed by the seed, counter {scene, (draw * PP_MAX_CARS + car) * 4 + q, 0x4D43}; Irwin-Hall of its
  * four 32-bit uniforms scaled to unit variance. */
 static double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, int q) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)((draw * 16 + car) * 4 + q), 0x4D43u};
+    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)((draw * PP_MAX_CARS + car) * 4 + q), 0x4D43u};
     for (int r = 0; r < 10; r++) {
         uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0], p1 = (uint64_t)0xCD9E8D57u * ctr[2];
         uint32_t n0 = (uint32_t)(p1 >> 32) ^ ctr[1] ^ key[0];
@@ -589,19 +589,21 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
     int nc = 0;
     int ncar = in->n_cars[s];
     if (ncar > in->car_stride) ncar = in->car_stride;
-    /* with a car table (the reference's persistent std::map, :1194): ids 0..PP_MAX_CARS-1 in
-     * order, each reported this frame (re-matched: slot overwritten, or erased, :1329-1348) or
-     * taken from its stale slot; without one: the frame's rows in (ascending id) order */
+    /* with a car table (the reference's persistent std::map, :1194): the tab_slots slots in order
+     * (ascending id, include/pp.h), each car reported this frame (re-matched: slot overwritten, or
+     * erased, :1329-1348) or taken from its stale slot; without one: the frame's rows in
+     * (ascending id) order */
     const int tab = in->tab_valid != NULL;
-    const int iters = tab ? PP_MAX_CARS : ncar;
+    const int iters = tab ? in->tab_slots : ncar;
     int p = 0;
     for (int it = 0; it < iters; it++) {
         int row = it;
-        if (tab) {
-            while (p < ncar && in->car_id[(int64_t)p * S + s] < it) p++;
-            row = (p < ncar && in->car_id[(int64_t)p * S + s] == it) ? p++ : -1;
-        }
         const int64_t tix = (int64_t)it * S + s;
+        const int sid = tab ? (in->tab_id ? in->tab_id[tix] : it) : 0;
+        if (tab) {
+            while (p < ncar && in->car_id[(int64_t)p * S + s] < sid) p++;
+            row = (p < ncar && in->car_id[(int64_t)p * S + s] == sid) ? p++ : -1;
+        }
         OCar c;
         memset(&c, 0, sizeof(c));
         if (row >= 0) {
@@ -633,7 +635,7 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
             }
         } else {
             if (!in->tab_valid[tix]) continue;
-            c.id = it;
+            c.id = sid;
             c.lane = in->tab_lane[tix];
             c.s = in->tab_s[tix]; c.d = in->tab_d[tix]; c.vs = in->tab_vs[tix]; c.vd = in->tab_vd[tix];
             c.vx = in->tab_vx[tix]; c.vy = in->tab_vy[tix];
@@ -652,24 +654,28 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
         if (diff > 6.0) { T = ego_lane; pr->status |= PP_ST_TOO_FAR; }
     }
     /* follow-car selection (:1383-1411), for the in-lane car and for every candidate lane */
-    int in_k = -1;
+    /* the reference tracks the chosen car by its id with -1 as "none" (:1383-1411): a car whose id
+     * is -1 is chosen and still reads as none, so the next qualifying car replaces it and no
+     * limit follows it; the ids are what :1411 compares */
+    int in_id = -1, in_k = -1;
     double in_s = 0;
-    int tk[PP_NUM_LANES];
+    int t_id[PP_NUM_LANES], tk[PP_NUM_LANES];
     double ts_[PP_NUM_LANES];
-    for (int L = 0; L < PP_NUM_LANES; L++) { tk[L] = -1; ts_[L] = 0; }
+    for (int L = 0; L < PP_NUM_LANES; L++) { t_id[L] = -1; tk[L] = -1; ts_[L] = 0; }
     for (int k = 0; k < nc; k++) {
         double s0 = cars[k].s + cars[k].vs * pr->dt0;
         double d0 = cars[k].d + cars[k].vd * pr->dt0;
         if (s0 > ego_s && fabs(d0 - ego_d) < 3) {
-            if (in_k == -1 || in_s > s0) { in_k = k; in_s = s0; }
+            if (in_id == -1 || in_s > s0) { in_id = cars[k].id; in_k = k; in_s = s0; }
         }
         for (int L = 0; L < PP_NUM_LANES; L++) {
             if (s0 >= ego_s - P->car_length - P->safety_distance && fabs(d0 - lane_offset(L)) < 3) {
-                if (tk[L] == -1 || ts_[L] > s0) { tk[L] = k; ts_[L] = s0; }
+                if (t_id[L] == -1 || ts_[L] > s0) { t_id[L] = cars[k].id; tk[L] = k; ts_[L] = s0; }
             }
         }
     }
-    pr->in_id = in_k >= 0 ? cars[in_k].id : -1;
+    if (in_id == -1) in_k = -1;
+    pr->in_id = in_id;
     int col = 0, code;
     if (in_k >= 0) {                                                    /* :1425-1431 */
         pr->has_in = 1;
@@ -677,7 +683,7 @@ static void prep_scene(const OMap* m, const pp_params* P, const pp_scene_batch* 
         pr->status |= limit_flag[code] | (col ? PP_ST_COLLISION : 0);
     }
     for (int L = 0; L < PP_NUM_LANES; L++) {                            /* :1411, 1432-1438 */
-        if (tk[L] >= 0 && in_k >= 0 && cars[tk[L]].id == cars[in_k].id) tk[L] = -1;
+        if (t_id[L] == -1 || t_id[L] == in_id) tk[L] = -1;
         pr->has_l[L] = tk[L] >= 0;
         if (tk[L] >= 0) {
             code = limit_speed(P, &cars[tk[L]], ts_[L], ego_s, ego_speed, ego_acc, 0, &pr->l_ts[L], &pr->l_tt[L], &col);

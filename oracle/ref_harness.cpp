@@ -356,3 +356,36 @@ extern "C" int ref_rollout(const double* wx, const double* wy, int n_wp, pp_scen
     }
     return 0;
 }
+
+// ---- one episode, frame by frame (the reference lambda's state across calls) -----------------
+// A session holds what main() holds across onMessage calls: the Map (with its mutable frame
+// members), the std::map<int, Car> sensor_fusion_cars (:1194) and target_lane (:1195). Each call
+// runs one telemetry frame (scene 0 of `in`, any car ids) and returns the frame's next_x/next_y.
+struct RefSession {
+    Map map;
+    std::map<int, Car> cars;
+    int target_lane;
+};
+
+extern "C" void* ref_session_new(const double* wx, const double* wy, int n_wp, int target_lane) {
+    RefSession* h = new RefSession();
+    vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
+    h->map.Init(X, Y);
+    h->target_lane = target_lane;
+    return h;
+}
+
+extern "C" int ref_session_frame(void* hp, const pp_scene_batch* in, double* next_xy, int* n_out,
+                                 int* target_lane, int* n_table) {
+    RefSession* h = (RefSession*)hp;
+    vector<Point> P;
+    refh::rollout_frame(h->map, h->cars, in, 0, h->target_lane, P);
+    const int n = (int)P.size() < 50 ? (int)P.size() : 50;
+    for (int i = 0; i < n; i++) { next_xy[2 * i] = P[i].x; next_xy[2 * i + 1] = P[i].y; }
+    *n_out = n;
+    *target_lane = h->target_lane;
+    *n_table = (int)h->cars.size();
+    return 0;
+}
+
+extern "C" void ref_session_free(void* hp) { delete (RefSession*)hp; }

@@ -97,6 +97,44 @@ def load_ref():
     return lib
 
 
+def load_ref_session():
+    """The reference's own frame code with main()'s cross-frame state (ref_session_*), or None."""
+    lib = load_ref()
+    if lib is None:
+        return None
+    lib.ref_session_new.argtypes = [_dp, _dp, C.c_int, C.c_int]
+    lib.ref_session_new.restype = C.c_void_p
+    lib.ref_session_frame.argtypes = [C.c_void_p, C.POINTER(ppamd.SceneBatch), _dp, C.POINTER(C.c_int),
+                                      C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    lib.ref_session_free.argtypes = [C.c_void_p]
+    return lib
+
+
+def _arr(a):
+    """float64 ctypes pointer to a (kept alive by the caller's reference to a)."""
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_dp)
+
+
+def one_scene(ego, prev, rows, target_lane):
+    """A host batch of one telemetry frame (ego x, y, yaw_deg, speed_mph; previous points (n, 2);
+    sensor_fusion rows (id, x, y, vx, vy) in the order sent); returns {"struct", arrays...}."""
+    J = max(len(rows), 1)
+    d = ppamd.alloc_scenes(1, J)
+    d["ego_x"][0], d["ego_y"][0], d["ego_yaw_deg"][0], d["ego_speed_mph"][0] = ego
+    n = min(len(prev), ppamd.PREV_KEEP)
+    d["n_prev"][0] = len(prev)
+    d["prev_x"][:n, 0] = [p[0] for p in prev[:n]]
+    d["prev_y"][:n, 0] = [p[1] for p in prev[:n]]
+    d["prev_target_lane"][0] = target_lane
+    d["n_cars"][0] = len(rows)
+    for j, (cid, x, y, vx, vy) in enumerate(rows):
+        d["car_id"][j, 0] = cid
+        d["car_x"][j, 0], d["car_y"][j, 0], d["car_vx"][j, 0], d["car_vy"][j, 0] = x, y, vx, vy
+    d["struct"] = ppamd.scene_struct(d)
+    return d
+
+
 def copy_state(scenes, traffic):
     return ({k: np.array(v, copy=True) for k, v in scenes.items()},
             {k: (np.array(v, copy=True) if isinstance(v, np.ndarray) else v) for k, v in traffic.items()})

@@ -1,0 +1,192 @@
+"""Sensor-fusion car tables of any size and any int ids (the reference's std::map<int, Car>
+sensor_fusion_cars, src/main.cpp:1194, 1325-1350, and its id -1 "no car" sentinel at :1383-1432).
+
+- CPU: the C restatement equals the reference's own code on frames with 24 rows and ids that are
+  negative (-1 included), sparse and large.
+- GPU: pp_eval with 24 rows against the restatement; pp_plan_frame (the host std::map laid out as
+  table slots over the union of the stored and reported ids, csrc/pp_cartable.h) driven through
+  closed-loop episodes next to a reference session that keeps the real std::map — 24 cars with ids
+  >= 16, a sensor range that leaves stale entries, cars dropping out of the road (erased), and ids
+  that include -1."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import ppamd
+
+
+def many_car_scenes(m, S, seed, ids_fn):
+    """S synthetic scenes with 24 sensor_fusion rows: two generator batches' cars side by side,
+    rows reordered by the ids ids_fn(rng, 24) (ascending, as the batch contract requires)."""
+    a = ppamd.synth_host(m, S, seed=seed, first=0)
+    b = ppamd.synth_host(m, S, seed=seed + 1, first=0)
+    sc = {k: v for k, v in a.items()}
+    for k in ("car_x", "car_y", "car_vx", "car_vy"):
+        sc[k] = np.ascontiguousarray(np.concatenate([a[k], b[k]], 0))
+    rng = np.random.default_rng(seed)
+    ids = np.zeros((24, S), np.int32)
+    for s in range(S):
+        ids[:, s] = np.sort(ids_fn(rng, 24))
+    sc["car_id"] = ids
+    sc["n_cars"] = np.full(S, 24, np.int32)
+    sc["n_cars"][::7] = 19
+    return sc
+
+
+def ids_wide(rng, n):
+    """distinct ascending ints: negatives (-1 in about half the scenes), sparse, up to 2^30"""
+    pool = np.concatenate([rng.choice(np.arange(-40, 0), 3, replace=False),
+                           rng.choice(np.arange(16, 2 ** 30, 9973), n, replace=False)])
+    if rng.random() < 0.5:
+        pool[0] = -1
+    return rng.choice(np.unique(pool), n, replace=False)
+
+
+def test_restatement_equals_reference_many_cars():
+    rlib = oracle_lib.load_ref()
+    olib = oracle_lib.load_oracle()
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    sc = many_car_scenes(m, 600, 4711, ids_wide)
+    prm = ppamd.default_params(n_speeds=5)
+    ref = oracle_lib.ref_eval(rlib, wx, wy, sc, 5, [prm.speed_offsets[i] for i in range(4)])
+    got = oracle_lib.oracle_eval(olib, wx, wy, sc, ppamd.default_params(n_speeds=5, emit_paths=True), info=True)
+    assert np.array_equal(np.stack([got["next_x"].T, got["next_y"].T], -1), ref["ref_next"])
+    assert np.array_equal(got["n_out"], ref["ref_n"])
+    gp = np.transpose(got["paths"], (0, 2, 1, 3))
+    assert np.array_equal(np.nan_to_num(gp, nan=7e7), np.nan_to_num(ref["paths"], nan=7e7))
+    # the -1 sentinel matters on some scenes: a car with id -1 was the nearest in-lane car
+    assert (got["info"]["in_lane_car"] == -1).sum() > 0
+
+
+# ---- closed-loop episodes through pp_plan_frame -------------------------------------------------
+class Traffic:
+    """Cars following lane centre polylines (map geometry), seeded; ids given."""
+
+    def __init__(self, geom, ids, rng, ego_s0):
+        self.lc = [geom[:, 4 + 2 * L:6 + 2 * L] for L in range(ppamd.NUM_LANES)]
+        seg = [np.hypot(*np.diff(np.vstack([c, c[:1]]), axis=0).T) for c in self.lc]
+        self.cum = [np.concatenate([[0], np.cumsum(s)]) for s in seg]
+        self.ids = list(ids)
+        n = len(ids)
+        self.lane = rng.integers(0, ppamd.NUM_LANES, n)
+        self.s = (ego_s0 + rng.uniform(-60, 260, n)) % self.cum[0][-1]
+        self.v = rng.uniform(4, 26, n)
+        self.off = rng.uniform(-0.4, 0.4, n)
+        self.leave = rng.random(n) < 0.25           # leave the road after frame 40 (matching fails > 1 km off)
+
+    def pos(self, j):
+        L = self.lane[j]
+        c, cum = self.lc[L], self.cum[L]
+        s = self.s[j] % cum[-1]
+        i = int(np.searchsorted(cum, s, side="right") - 1)
+        a, b = c[i % len(c)], c[(i + 1) % len(c)]
+        t = (s - cum[i]) / (cum[i + 1] - cum[i])
+        u = (b - a) / np.hypot(*(b - a))
+        p = a + t * (b - a) + self.off[j] * np.array([u[1], -u[0]])
+        return p, u * self.v[j]
+
+    def step(self, dt, f):
+        self.s += self.v * dt
+        self.off = np.where(self.leave & (f > 40), self.off + 60.0, self.off)
+
+
+def run_episode(env, ids, frames, seed, sensor_range):
+    m, wx, wy = env["m"], env["wx"], env["wy"]
+    rlib = env["rlib"]
+    geom = m.geometry()
+    rng = np.random.default_rng(seed)
+    # ego starts on a lane centre with a previous path along it
+    sc = ppamd.synth_host(m, 1, seed=seed, first=0)
+    ego = [float(sc["ego_x"][0]), float(sc["ego_y"][0]), float(sc["ego_yaw_deg"][0]), float(sc["ego_speed_mph"][0])]
+    prev = np.stack([sc["prev_x"][:, 0], sc["prev_y"][:, 0]], 1)
+    n_prev = int(sc["n_prev"][0])
+    traffic = Traffic(geom, ids, rng, 0.0)
+    # place the traffic near the ego: shift each car's s so it starts within the sensor window
+    ego_pt = np.array(ego[:2])
+    for j in range(len(ids)):
+        c, cum = traffic.lc[traffic.lane[j]], traffic.cum[traffic.lane[j]]
+        k = int(np.argmin(np.hypot(*(c - ego_pt).T)))
+        traffic.s[j] = (cum[k] + rng.uniform(-50, 200)) % cum[-1]
+    ppamd.plan_reset(m)
+    h = rlib.ref_session_new(oracle_lib._arr(wx), oracle_lib._arr(wy), len(wx), 1)
+    tl_gpu = 1
+    worst, stale, erased, reported_max = 0.0, 0, 0, 0
+    try:
+        for f in range(frames):
+            rows = []
+            for j, cid in enumerate(traffic.ids):
+                p, v = traffic.pos(j)
+                if np.hypot(*(p - np.array(ego[:2]))) <= sensor_range:
+                    rows.append((cid, p[0], p[1], v[0], v[1]))
+            reported_max = max(reported_max, len(rows))
+            # reference session (one scene, rows in any order: the reference iterates them as sent)
+            order = rng.permutation(len(rows))
+            rows_sent = [rows[i] for i in order]
+            one = oracle_lib.one_scene(ego, prev[:n_prev], rows_sent, tl_gpu)
+            nxy = np.zeros(100)
+            n_out = C.c_int()
+            tl_ref = C.c_int()
+            ntab = C.c_int()
+            rlib.ref_session_frame(h, C.byref(one["struct"]), nxy.ctypes.data_as(oracle_lib._dp), C.byref(n_out),
+                                   C.byref(tl_ref), C.byref(ntab))
+            nx, ny, tl_gpu = ppamd.plan_frame(m, ego[0], ego[1], ego[2], ego[3], prev[:n_prev, 0], prev[:n_prev, 1],
+                                              rows_sent, target_lane=tl_gpu)
+            n = n_out.value
+            assert len(nx) == n and tl_gpu == tl_ref.value, (f, len(nx), n, tl_gpu, tl_ref.value)
+            ref_xy = nxy[:2 * n].reshape(n, 2)
+            if n:
+                worst = max(worst, float(np.abs(np.stack([nx, ny], 1) - ref_xy).max()))
+            assert worst <= oracle_lib.TOL, (f, worst)
+            stale += ntab.value > len(rows)
+            erased += ntab.value < len(rows)
+            # drive 3 points of the plan
+            plan = ref_xy
+            k = min(3, n)
+            if k >= 1:
+                q = plan[k - 2] if k >= 2 else np.array(ego[:2])
+                d = plan[k - 1] - q
+                ego = [plan[k - 1][0], plan[k - 1][1],
+                       float(np.degrees(np.arctan2(d[1], d[0]))) if np.hypot(*d) > 0 else ego[2],
+                       float(np.hypot(*d) * 50 * 2.237)]
+            prev = plan[k:]
+            n_prev = len(prev)
+            traffic.step(0.02 * max(k, 1), f)
+    finally:
+        rlib.ref_session_free(h)
+    return worst, stale, erased, reported_max
+
+
+@pytest.mark.gpu
+class TestCarTableGPU:
+    @pytest.fixture(scope="class")
+    def env(self):
+        import torch
+        wx, wy = oracle_lib.highway_map()
+        return {"torch": torch, "m": ppamd.Map(wx, wy), "wx": wx, "wy": wy, "dev": torch.device("cuda", 0),
+                "olib": oracle_lib.load_oracle(), "rlib": oracle_lib.load_ref_session()}
+
+    def test_eval_many_cars_vs_oracle(self, env):
+        sc = many_car_scenes(env["m"], 1500, 99, ids_wide)
+        for mode in (ppamd.COST_REFERENCE, ppamd.COST_COMFORT):
+            prm = ppamd.default_params(emit_paths=True, cost_mode=mode)
+            d = {k: env["torch"].from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
+            r = ppamd.alloc_result(1500, prm, xp="torch", device=env["dev"])
+            ppamd.evaluate(env["m"], d, prm, r, device=0)
+            env["torch"].cuda.synchronize()
+            got = ppamd.result_to_numpy(r)
+            ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+            oracle_lib.compare(got, ref)
+
+    @pytest.mark.parametrize("ids,sensor_range,seed,need", [
+        (list(range(1000, 1000 + 7 * 24, 7)), 60.0, 3, "stale"),   # 24 cars, ids >= 16, stale entries
+        (sorted([-1, -9, 5, 17, 64, 99999, 2 ** 31 - 2, 12, 300, 301, 40, 41]), 1e5, 5, "erased"),
+        (list(range(16, 40)), 45.0, 8, "stale"),
+    ])
+    def test_plan_frame_episode_vs_reference(self, env, ids, sensor_range, seed, need):
+        worst, stale, erased, rep = run_episode(env, ids, 300, seed, sensor_range)
+        print(f"ids {ids[:3]}..: max |dxy| {worst:.3e} m, frames with stale entries {stale}, "
+              f"with erased {erased}, max reported {rep}")
+        assert (stale if need == "stale" else erased) > 0

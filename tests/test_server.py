@@ -58,9 +58,10 @@ def test_protocol_without_telemetry(m):
     assert rc == 0 and stats[0] == 0 and stats[2] >= 3 and stats[3] >= 7
 
 
-def episode_frames(olib, wx, wy, F, first_scene):
+def episode_frames(olib, wx, wy, F, first_scene, id_of=lambda j: j):
     """Telemetry frames of a closed-loop episode from the restatement (one scene), rendered as
-    the simulator would send them, with the restatement's plan for each."""
+    the simulator would send them (car j reported with id id_of(j), an increasing map), with the
+    restatement's plan for each."""
     sc, tr = ppamd.synth_traffic_host(ppamd.Map(wx, wy), 1, seed=0x5EED0007, first=first_scene)
     sc["prev_target_lane"][:] = 1           # the lambda's target_lane starts at 1 (src/main.cpp:1195)
     prm = ppamd.default_params(n_speeds=1)
@@ -72,7 +73,7 @@ def episode_frames(olib, wx, wy, F, first_scene):
         plans.append((lg["plan_x"][0, :n, 0], lg["plan_y"][0, :n, 0]))
         npv = min(int(tel["n_prev"][0]), 10)
         fmt = lambda a: ",".join(repr(float(v)) for v in a)
-        rows = ",".join("[%d,%r,%r,%r,%r,0,0]" % (int(tel["car_id"][j, 0]), float(tel["car_x"][j, 0]),
+        rows = ",".join("[%d,%r,%r,%r,%r,0,0]" % (id_of(int(tel["car_id"][j, 0])), float(tel["car_x"][j, 0]),
                                                    float(tel["car_y"][j, 0]), float(tel["car_vx"][j, 0]),
                                                    float(tel["car_vy"][j, 0])) for j in range(int(tel["n_cars"][0])))
         frames.append(('42["telemetry",{"x":%r,"y":%r,"yaw":%r,"speed":%r,"s":0,"d":0,"previous_path_x":[%s],'
@@ -84,13 +85,16 @@ def episode_frames(olib, wx, wy, F, first_scene):
 
 
 @pytest.mark.gpu
-def test_served_episodes_match_restatement(m):
+@pytest.mark.parametrize("id_of", [lambda j: j, lambda j: 1000 + 37 * j], ids=["ids0-11", "ids1000+"])
+def test_served_episodes_match_restatement(m, id_of):
     """Four simulators in parallel, 60 frames each: every reply equals the restatement's plan of
-    that frame within 1e-6 m (the car table and target lane persist per connection)."""
+    that frame within 1e-6 m (the car table and target lane persist per connection). With ids
+    1000 + 37 j the connection's std::map holds ids far beyond the table's slot count: the plans
+    are the same (the reference orders cars by id and compares ids, nothing else)."""
     wx, wy = oracle_lib.highway_map()
     olib = oracle_lib.load_oracle()
     K, F = 4, 60
-    eps = [episode_frames(olib, wx, wy, F, k) for k in range(K)]
+    eps = [episode_frames(olib, wx, wy, F, k, id_of) for k in range(K)]
     srv = ppamd.Server(m, max_clients=K)
     try:
         cl = [WSClient(srv.port.value) for _ in range(K)]
