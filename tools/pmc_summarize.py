@@ -34,7 +34,14 @@ if tag:
     fetch = kc.get("FETCH_SIZE")
     write = kc.get("WRITE_SIZE")
     if fetch is not None and write is not None:
+        # every kernel of one evaluation (k_prep, both k_cand instantiations, k_emit / k_winner):
+        # the step's whole HBM traffic, beside k_cand's own
+        per_kernel = {k: (2 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)) * 1024.0
+                      for k, v in summary.items()
+                      if k.split("<")[0] in ("k_prep", "k_cand", "k_emit", "k_winner")}
         out[tag] = {"hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
+                    "pipeline_bytes_per_step": sum(per_kernel.values()),
+                    "pipeline_bytes_by_kernel": per_kernel,
                     "fetch_kib_raw": fetch, "write_kib": write,
                     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), k_cand instantiations summed",
                     "counters": kc}
