@@ -72,18 +72,11 @@ __device__ __forceinline__ double distsq_pt_seg(double px, double py, double ax,
     return snom * snom / rdenom;
 }
 
-// Map::init_reference_waypoint (src/main.cpp:143-197)
-__device__ inline void init_reference_waypoint(const MapV& m, double x, double y, int& ref_wp,
-                                               double ratio[NL]) {
+// Map::init_reference_waypoint (src/main.cpp:143-197) from the closest waypoint on (:150-154 done
+// by the caller)
+__device__ inline void init_reference_waypoint_from(const MapV& m, double x, double y, int closest,
+                                                    int& ref_wp, double ratio[NL]) {
     const int n = m.n;
-    int closest = 0;
-    double cd;
-    { const double dx = m.ref_x[0] - x, dy = m.ref_y[0] - y; cd = dx * dx + dy * dy; }
-    for (int i = 1; i < n; i++) {
-        const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
-        const double d = dx * dx + dy * dy;
-        if (d < cd) { closest = i; cd = d; }
-    }
     double rnom, snom, rdenom, d0, d1;
     {
         const int a = wpi(closest - 1, n), b = wpi(closest, n), c = wpi(closest + 1, n);
@@ -105,6 +98,48 @@ __device__ inline void init_reference_waypoint(const MapV& m, double x, double y
                       m.lc_y[lane * n + b], rnom, rdenom, snom);
         ratio[lane] = rnom / rdenom;
     }
+}
+
+// Map::init_reference_waypoint (src/main.cpp:143-197)
+__device__ inline void init_reference_waypoint(const MapV& m, double x, double y, int& ref_wp,
+                                               double ratio[NL]) {
+    const int n = m.n;
+    int closest = 0;
+    double cd;
+    { const double dx = m.ref_x[0] - x, dy = m.ref_y[0] - y; cd = dx * dx + dy * dy; }
+    for (int i = 1; i < n; i++) {
+        const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
+        const double d = dx * dx + dy * dy;
+        if (d < cd) { closest = i; cd = d; }
+    }
+    init_reference_waypoint_from(m, x, y, closest, ref_wp, ratio);
+}
+
+// The same, the closest-waypoint scan (:150-154: the first i with the smallest |ref_i - p|^2 under
+// `d < cd` from cd = d_0) split over the G lanes of a group (lane r scans i = r, r + G, ...) and
+// reduced by (distance, index). Equal to the serial scan: a NaN d_i never wins `d < cd`, a NaN d_0
+// keeps waypoint 0, and no finite-or-infinite d below d_0 keeps waypoint 0 as well.
+template <int G>
+__device__ inline void init_reference_waypoint_grp(const MapV& m, double x, double y, int r,
+                                                   int& ref_wp, double ratio[NL]) {
+    const int n = m.n;
+    int closest = -1;
+    double cd = __builtin_inf();
+    for (int i = r; i < n; i += G) {
+        const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
+        const double d = dx * dx + dy * dy;
+        if (d < cd) { closest = i; cd = d; }
+    }
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        const double od = __shfl_xor(cd, o, G);
+        const int oc = __shfl_xor(closest, o, G);
+        if (oc >= 0 && (closest < 0 || od < cd || (od == cd && oc < closest))) { cd = od; closest = oc; }
+    }
+    const double dx0 = m.ref_x[0] - x, dy0 = m.ref_y[0] - y;
+    const double d0 = dx0 * dx0 + dy0 * dy0;
+    if (closest < 0 || !(d0 == d0) || !(cd < d0)) closest = 0;
+    init_reference_waypoint_from(m, x, y, closest, ref_wp, ratio);
 }
 
 // Map::lane_matching (src/main.cpp:199-275); bounded walk (never reached on finite input).

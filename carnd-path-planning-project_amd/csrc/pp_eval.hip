@@ -18,6 +18,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -40,6 +42,34 @@ __device__ __forceinline__ void diag(int k, bool c) {
 #define PP_DIAGC(k, c) diag(k, c)
 #else
 #define PP_DIAGC(k, c) ((void)0)
+#endif
+#ifdef PP_CHECK
+// checking builds only (-DPP_CHECK): every global store of k_cand / k_emit (and the record reads
+// of k_emit) is tested against the buffer it belongs to, and k_cand poisons its LDS slots at the
+// start of every group, so a slot read that phase A of the same group did not write shows up as a
+// NaN result or a meta sentinel. g_chk: [0] violations, [1] first site, [2] its offset, [3] its
+// workgroup, [4] its group. Read with pp_check_read.
+struct ChkLim {
+    const double *paths, *nx, *ny, *rec, *cost;
+    const unsigned long long* adjm;
+    long long npaths, nnext, nrec, nadj, ncost, nscen;
+};
+__device__ unsigned long long g_chk[8];
+__device__ ChkLim g_lim;
+__device__ __forceinline__ bool chk_(bool ok, int site, long long off, long long grp) {
+    if (!ok && atomicAdd(&g_chk[0], 1ull) == 0ull) {
+        g_chk[1] = (unsigned long long)site; g_chk[2] = (unsigned long long)off;
+        g_chk[3] = blockIdx.x; g_chk[4] = (unsigned long long)grp;
+    }
+    return ok;
+}
+// p inside [g_lim.B, g_lim.B + g_lim.N)
+#define PP_CHKP(p, B, N, site) chk_((const void*)(p) >= (const void*)g_lim.B && (const void*)(p) < (const void*)(g_lim.B + g_lim.N), site, (long long)((const char*)(p) - (const char*)g_lim.B), -1)
+#define PP_CHK(ok, site, off) chk_((ok), site, (long long)(off), -1)
+constexpr int kMetaPoison = 0x7fffffff;
+#else
+#define PP_CHKP(p, B, N, site) true
+#define PP_CHK(ok, site, off) true
 #endif
 #include "pp_device.h"
 #include "pp_glibcm.h"
@@ -101,6 +131,9 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_CAR_SORT
 #define PP_CAR_SORT 1
 #endif
+#ifndef PP_CAR_SORT_BATCH
+#define PP_CAR_SORT_BATCH 0
+#endif
 // standing candidates (speed 0) take the turn series whatever the angle
 #ifndef PP_STAND_SERIES
 #define PP_STAND_SERIES 0
@@ -145,6 +178,334 @@ __device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_
 // k_cand groups (SPB scenes per group, or BPS groups per scene): k_prep marks the groups holding a
 // kLimSlow scene in this bitmap for k_cand<true>
 struct GroupBits { uint32_t* bits; int SPB, BPS; };
+// ---- K1 building blocks, shared by k_prep (one lane per evaluation) and k_prep_g2..16 (G lanes) ----
+
+// Ego state of one evaluation: derivation (src/main.cpp:1233-1292), Frenet frame and ego matching
+// (:1299-1320).
+struct EgoSt {
+    double ego_x, ego_y, yaw, ego_speed, ego_acc, esv_x, esv_y, dt0, p8x, p8y;
+    double ego_s, ego_d, ego_vs, ego_vd, ratio[NL];
+    int K, ref_wp, ego_lane;
+    uint32_t status;
+};
+
+// G > 1: the G lanes of a group (this one is lane r) split the reference-waypoint scan; every
+// lane ends with the same state
+template <int G>
+__device__ __forceinline__ void prep_ego(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                         int64_t S, int64_t s, int r, EgoSt& e) {
+    e.status = 0;
+    e.ego_x = in.ego_x[s]; e.ego_y = in.ego_y[s];
+    e.yaw = in.ego_yaw_deg[s];
+    double ego_speed = in.ego_speed_mph[s];
+    ego_speed /= 2.237;
+    e.ego_acc = 0; e.esv_x = 0; e.esv_y = 0; e.dt0 = 0;
+    e.K = 0;
+    e.p8x = 0; e.p8y = 0;
+    if (in.n_prev[s] >= PP_PREV_KEEP) {
+        e.K = PP_PREV_KEEP;
+        const double p7x = in.prev_x[7 * S + s], p7y = in.prev_y[7 * S + s];
+        e.p8x = in.prev_x[8 * S + s]; e.p8y = in.prev_y[8 * S + s];
+        const double p9x = in.prev_x[9 * S + s], p9y = in.prev_y[9 * S + s];
+        const double ax = e.p8x - p7x, ay = e.p8y - p7y;
+        const double v2 = sqrt(ax * ax + ay * ay);
+        e.esv_x = p9x - e.p8x; e.esv_y = p9y - e.p8y;
+        const double v3 = sqrt(e.esv_x * e.esv_x + e.esv_y * e.esv_y);
+        e.ego_acc = (v3 - v2) * 50;
+        ego_speed = v3 * 50;
+        e.esv_x *= 50; e.esv_y *= 50;
+        e.ego_x = p9x; e.ego_y = p9y;
+        e.dt0 = PP_PREV_KEEP / 50.0;
+    }
+    e.ego_speed = ego_speed;
+    if (G == 1) init_reference_waypoint(m, e.ego_x, e.ego_y, e.ref_wp, e.ratio);
+    else init_reference_waypoint_grp<G>(m, e.ego_x, e.ego_y, r, e.ref_wp, e.ratio);
+    e.ego_s = 0; e.ego_d = 0;
+    e.ego_lane = 0;
+    int nwp_unused = 0;
+    if (!lane_match(m, e.ref_wp, e.ratio, e.ego_x, e.ego_y, e.ego_s, e.ego_d, e.ego_lane, nwp_unused)) {
+        e.ego_s = e.ego_d = 0;
+        e.ego_lane = 0;
+        e.status |= PP_ST_EGO_UNMATCHED;
+    }
+    project_speed(m, e.esv_x, e.esv_y, e.ref_wp, e.ego_vs, e.ego_vd);
+    if (e.ego_acc > P.maximum_acc) e.ego_acc = P.maximum_acc;
+    if (e.ego_acc < -P.maximum_acc) e.ego_acc = -P.maximum_acc;
+}
+
+// LaneChangePlanner's accumulation (src/main.cpp:377-445) and the follow-car selection
+// (:1388-1410): order-dependent reductions over one car sequence. Every one is a minimum with ties
+// to the lower iteration index (or an AND / a count), so a visiting order other than ascending
+// ids gives the reference's result once ties compare that index explicitly — except for a chosen
+// car whose id is the reference's 'no car' sentinel -1, which any later car replaces: such
+// scenes (and car tables) are visited in iteration order.
+// (Per-lane state is indexed by the car's lane through selects, sel/put: a dynamically indexed
+// member array would live in scratch memory.)
+// (each element passes an empty asm first: a select chain over the array's own elements is
+// folded back into an indexed load, which puts the array in scratch memory)
+template <typename T>
+__device__ __forceinline__ T sel(const T (&a)[NL], int l) {
+    T x = a[0];
+    asm("" : "+v"(x));
+#pragma unroll
+    for (int i = 1; i < NL; i++) {
+        T ai = a[i];
+        asm("" : "+v"(ai));
+        x = l == i ? ai : x;
+    }
+    return x;
+}
+template <typename T>
+__device__ __forceinline__ void put(T (&a)[NL], int l, T x) {
+#pragma unroll
+    for (int i = 0; i < NL; i++) a[i] = l == i ? x : a[i];
+}
+struct PlanAcc {
+    int lane_speed[NL];                     // the int-truncated lane speed where bit l of ls_set
+    int ls_set;                             // (else P.max_speed)
+    double next_s[NL];
+    int open_m;                             // lane_open, bit l
+    int in_id; double in_s;
+    int t_id[NL];
+    double t_s[NL];
+    // iteration index of each running minimum, 6 bits each: next_s[l] at field l, the target-lane
+    // car of lane l at field NL + l, the in-lane car at field 2 NL (the follow cars' velocities are
+    // re-read from that index after the pass)
+    uint64_t its;
+    int nmatched;
+    __device__ __forceinline__ int it_of(int f) const { return (int)((its >> (6 * f)) & 63); }
+    __device__ __forceinline__ void set_it(int f, int it) { its = (its & ~(63ull << (6 * f))) | ((uint64_t)it << (6 * f)); }
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int l = 0; l < NL; l++) {
+            lane_speed[l] = 0; next_s[l] = 1000;
+            t_id[l] = -1; t_s[l] = 0;
+        }
+        open_m = (1 << NL) - 1;
+        ls_set = 0; in_id = -1; in_s = 0; its = 0; nmatched = 0;
+    }
+    // one matched car (iteration index it) with its Frenet state
+    __device__ __forceinline__ void add(const pp_params& P, const EgoSt& e, int T_in, int it, int id,
+                                        double cs, double cd, int clane, double cvs, double cvd) {
+        const double ego_s = e.ego_s, ego_vs = e.ego_vs, dt0 = e.dt0;
+        nmatched++;
+        // planner (src/main.cpp:379-444)
+        const double sp = cs + cvs * dt0;
+        if (sp > ego_s) {
+            // the first car (in iteration order) with the smallest sp sets next_s; lane_speed
+            // comes from it if it is within 200 m (an earlier, larger minimum never is then)
+            // (next_s == 1000: still the initial value, which no car can set, so it wins the tie)
+            const double ns = sel(next_s, clane);
+            if (sp < ns || (sp == ns && ns != 1000 && it < it_of(clane))) {
+                put(next_s, clane, sp);
+                set_it(clane, it);
+                if (sp - ego_s < 200) {
+                    int speed = (int)cvs;
+                    if (speed > P.max_speed) speed = (int)P.max_speed;
+                    if (sp - ego_s > 100)
+                        speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
+                    put(lane_speed, clane, speed);
+                    ls_set |= 1 << clane;
+                } else {
+                    ls_set &= ~(1 << clane);
+                }
+            }
+        }
+        bool open = true;
+        double add = 2;
+        if (T_in == clane) add = 0;
+        const double min_dist = P.car_length + P.safety_distance + add;
+        if (fabs(ego_s - sp) < min_dist) open = false;
+        if (sp > ego_s && cvs < ego_vs) {
+            const double car_dist = sp - ego_s - P.car_length - P.safety_distance - add;
+            const double sd = ego_vs - cvs;
+            const double dtm = sd / P.relaxed_acc;
+            const double ddist = ego_vs * dtm - sd / 2 * dtm;
+            if (car_dist < ddist) open = false;
+        }
+        if (sp < ego_s && cvs > ego_vs && sp + 50 > ego_s) {
+            const double car_dist = ego_s - sp - P.car_length - P.safety_distance - add;
+            const double sd = cvs - ego_vs;
+            double dtm = sd / P.relaxed_acc;
+            if (T_in == e.ego_lane) dtm += 2;
+            const double md = sd * dtm;
+            if (car_dist < md) open = false;
+        }
+        if (!open) open_m &= ~(1 << clane);
+        // follow cars (src/main.cpp:1391-1409); the target-lane choice for every candidate lane
+        const double s0 = cs + cvs * dt0;
+        const double d0 = cd + cvd * dt0;
+        if (s0 > ego_s && fabs(d0 - e.ego_d) < 3) {
+            if (in_id == -1 || in_s > s0 || (in_s == s0 && it < it_of(2 * NL))) {
+                in_id = id; in_s = s0; set_it(2 * NL, it);
+            }
+        }
+#pragma unroll
+        for (int L = 0; L < NL; L++) {
+            if (s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3) {
+                if (t_id[L] == -1 || t_s[L] > s0 || (t_s[L] == s0 && it < it_of(NL + L))) {
+                    t_id[L] = id; t_s[L] = s0; set_it(NL + L, it);
+                }
+            }
+        }
+    }
+};
+
+// OR / AND over the G lanes of a group
+template <int G>
+__device__ __forceinline__ uint32_t grp_or(uint32_t x) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o, G);
+    return x;
+}
+
+// The rest of K1 after the car pass (src/main.cpp:447-484, 1358-1438, 583-610, 786-823): scores
+// and the target lane, LimitSpeed for the in-lane car (task 0) and each lane's target car (task
+// 1 + L), k_cand<false>'s range checks, the build start pose and the frame rotations (tasks 0-3:
+// cos(-a), sin(-a), cos(a), sin(a)). G > 1: the tasks are spread over the lanes of the group
+// (lane r takes tasks r, r + G, ...) and lane 0 writes the scene's record.
+template <int G>
+__device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_params& P, const PrepV& pv,
+                                            pp_scene_info* info, uint32_t* out_status, const GroupBits& gb,
+                                            int64_t S, int64_t Sv, int64_t s, int64_t v, int draw, bool tab,
+                                            int r, int T_in, const EgoSt& e, const PlanAcc& a,
+                                            uint32_t status) {
+    // scores + argmax (src/main.cpp:447-484)
+    int best_lane = e.ego_lane;
+    double best_score = 0;
+    double score[NL];
+#pragma unroll
+    for (int lane = 0; lane < NL; lane++) {
+        score[lane] = 0;
+        if (lane != e.ego_lane && !((a.open_m >> lane) & 1)) continue;
+        const double lsp = ((a.ls_set >> lane) & 1) ? (double)a.lane_speed[lane] : P.max_speed;
+        const double speed_score = s_min(lsp / P.max_speed, 1.0);
+        const double distance_score = 1 - fabs((double)(T_in - lane)) / 2;
+        const double free_score = s_min(1.0, a.next_s[lane] / 100);
+        const double total = speed_score + distance_score / 2 + free_score;
+        score[lane] = total;
+        if (total > best_score) { best_score = total; best_lane = lane; }
+    }
+    int T;
+    if (abs(e.ego_lane - best_lane) > 1) {
+        const int nl = best_lane > e.ego_lane ? e.ego_lane + 1 : e.ego_lane - 1;
+        T = ((a.open_m >> nl) & 1) ? nl : e.ego_lane;
+        status |= PP_ST_JUMP_RULE;
+    } else {
+        T = best_lane;
+    }
+    const int open_mask = a.open_m;
+    if (open_mask != (1 << NL) - 1) status |= PP_ST_LANE_CLOSED;
+    if (T != e.ego_lane) {                                             // src/main.cpp:1358-1369
+        const double dtl = lane_offset(T);
+        const double diff = fabs(e.ego_vd * 1.0 + e.ego_d - dtl);
+        if (diff > 6.0) { T = e.ego_lane; status |= PP_ST_TOO_FAR; }
+    }
+    // LimitSpeed for the in-lane car and the per-lane target car (src/main.cpp:1411-1438); the
+    // reference's "no car" is id -1 (:1383-1432): a chosen car whose id is -1 reads as none; ids
+    // are what :1411 compares. k_cand<false> divides by reciprocals without range checks: every
+    // speed and ramp time of the scene must be in range (else kLimSlow)
+    int lim_mask = 0;
+    bool ok = true;
+    for (int t = r; t < 1 + NL; t += G) {
+        bool has = a.in_id != -1, in_lane = true;
+        double fs = a.in_s;
+        int fit = a.it_of(2 * NL);
+#pragma unroll
+        for (int L = 0; L < NL; L++)
+            if (t == 1 + L) { has = a.t_id[L] != -1 && a.t_id[L] != a.in_id; in_lane = false; fs = a.t_s[L]; fit = a.it_of(NL + L); }
+        if (!has) continue;
+        double ts, tt, fvx, fvy;
+        bool col;
+        car_velocity(in, P, S, s, draw, tab, fit, fvx, fvy);
+        const int code = limit_speed(P, fvx, fvy, fs, e.ego_s, e.ego_speed, e.ego_acc, in_lane, ts, tt, col);
+        status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
+        if (t == 0) { pv.in_ts[v] = ts; pv.in_tt[v] = tt; }
+        else { pv.l_ts[(t - 1) * Sv + v] = ts; pv.l_tt[(t - 1) * Sv + v] = tt; }
+        lim_mask |= 1 << t;
+        ok = ok && speed_in_range(ts) && speed_in_range(tt);
+    }
+    for (int k = r; k < P.n_speeds; k += G) {
+        const double vk = cand_speed(P, e.ego_speed, k);
+        ok = ok && speed_in_range(vk) && speed_in_range(fabs(e.ego_speed - vk) / P.relaxed_acc);
+    }
+    ok = ok && speed_in_range(e.ego_speed);
+    if (G > 1) {
+        status = grp_or<G>(status);
+        lim_mask = (int)grp_or<G>((uint32_t)lim_mask);
+        ok = grp_or<G>(ok ? 0u : 1u) == 0u;
+    }
+    // TrajectoryBuilder::build start pose (src/main.cpp:583-610) + frame rotations (:786-823)
+    double pos_x, pos_y, angle;
+    if (e.K == 0) {
+        pos_x = e.ego_x; pos_y = e.ego_y;
+        angle = e.yaw * kPi / 180;
+    } else {
+        pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
+        const double vx = pos_x - e.p8x, vy = pos_y - e.p8y;
+        if (vx * vx + vy * vy < kEps) angle = e.yaw * kPi / 180;
+        else angle = ppg::atan2(pos_y - e.p8y, pos_x - e.p8x);       // glibc's atan2, bit for bit
+    }
+    // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
+    // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
+    if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
+    if (!ok) lim_mask |= kLimSlow;
+    if ((lim_mask & kLimSlow) && r == 0) {
+        const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
+        for (int b = 0; b < gb.BPS; b++) atomicOr(&gb.bits[(g0 + b) >> 5], 1u << ((g0 + b) & 31));
+    }
+    // the frame's rotations cos(-angle), sin(-angle) (:786-787) and cos(angle), sin(angle)
+    // (:822-823) as the reference's libm computes them (pp_glibcm.h): every knot is a product with
+    // them, so the spline and every path position carry their exact bits. Headings of 1e8 rad and
+    // more (only from an absurd telemetry yaw) are outside the restated reduction.
+    double tv[4];
+    bool tfail = false;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        if (G > 1 && t % G != r) continue;
+        const double x = t < 2 ? -angle : angle;
+        tfail |= !((t & 1) ? ppg::sin(x, tv[t]) : ppg::cos(x, tv[t]));
+    }
+    if (G > 1) tfail = grp_or<G>(tfail ? 1u : 0u) != 0u;
+    if (tfail) {                              // every lane: both pairs (rare)
+        double sm, cm, sp, cp;
+        ppm::sincos_pp<true>(-angle, sm, cm);
+        ppm::sincos_pp<true>(angle, sp, cp);
+        tv[0] = cm; tv[1] = sm; tv[2] = cp; tv[3] = sp;
+    }
+    double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        if (G == 1 || t % G == r) tdst[t][v] = tv[t];
+    if (r != 0) return;
+    pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
+    pv.ego_speed[v] = e.ego_speed; pv.ego_d[v] = e.ego_d; pv.ego_vd[v] = e.ego_vd;
+#pragma unroll
+    for (int l = 0; l < NL; l++) { pv.ratio[l * Sv + v] = e.ratio[l]; pv.score[l * Sv + v] = score[l]; }
+    pv.K[v] = e.K; pv.ref_wp[v] = e.ref_wp; pv.T[v] = T; pv.ego_lane[v] = e.ego_lane;
+    pv.open_mask[v] = open_mask; pv.lim_mask[v] = lim_mask; pv.status[v] = status;
+    if (draw == 0) out_status[s] = 0;        // k_cand ORs its flags in (atomics when a scene spans blocks)
+    if (info && draw == 0) {
+        pp_scene_info I = {};
+        I.ego_x = e.ego_x; I.ego_y = e.ego_y; I.ego_speed = e.ego_speed; I.ego_acc = e.ego_acc;
+        I.ego_s = e.ego_s; I.ego_d = e.ego_d; I.ego_vs = e.ego_vs; I.ego_vd = e.ego_vd;
+        for (int l = 0; l < NL; l++) { I.ref_ratio[l] = e.ratio[l]; I.lane_score[l] = score[l]; }
+        I.ref_wp = e.ref_wp; I.ego_lane = e.ego_lane; I.target_lane = T; I.lane_open_mask = open_mask;
+        I.n_matched_cars = a.nmatched; I.in_lane_car = a.in_id;
+        info[s] = I;
+    }
+}
+
+// Monte-Carlo sensor noise on one car row (include/pp.h pp_params)
+__device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int draw, int row, double& cx,
+                                          double& cy, double& cvx, double& cvy) {
+    const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+    cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 0);
+    cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 1);
+    cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 2);
+    cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
+}
+
 template <bool kLdsMap>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
@@ -165,63 +526,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     const int64_t s = D == 1 ? v : v / D;
     const int draw = (int)(v - s * D);
 
-    uint32_t status = 0;
-    // ---- ego derivation (src/main.cpp:1233-1292) ----
-    double ego_x = in.ego_x[s], ego_y = in.ego_y[s];
-    const double yaw = in.ego_yaw_deg[s];
-    double ego_speed = in.ego_speed_mph[s];
-    ego_speed /= 2.237;
-    double ego_acc = 0, esv_x = 0, esv_y = 0, dt0 = 0;
-    int K = 0;
-    double p8x = 0, p8y = 0;
-    if (in.n_prev[s] >= PP_PREV_KEEP) {
-        K = PP_PREV_KEEP;
-        const double p7x = in.prev_x[7 * S + s], p7y = in.prev_y[7 * S + s];
-        p8x = in.prev_x[8 * S + s]; p8y = in.prev_y[8 * S + s];
-        const double p9x = in.prev_x[9 * S + s], p9y = in.prev_y[9 * S + s];
-        const double ax = p8x - p7x, ay = p8y - p7y;
-        const double v2 = sqrt(ax * ax + ay * ay);
-        esv_x = p9x - p8x; esv_y = p9y - p8y;
-        const double v3 = sqrt(esv_x * esv_x + esv_y * esv_y);
-        ego_acc = (v3 - v2) * 50;
-        ego_speed = v3 * 50;
-        esv_x *= 50; esv_y *= 50;
-        ego_x = p9x; ego_y = p9y;
-        dt0 = PP_PREV_KEEP / 50.0;
-    }
-    // ---- Frenet frame + ego matching (src/main.cpp:1299-1320) ----
-    int ref_wp;
-    double ratio[NL];
-    init_reference_waypoint(m, ego_x, ego_y, ref_wp, ratio);
-    double ego_s = 0, ego_d = 0;
-    int ego_lane = 0, nwp_unused = 0;
-    if (!lane_match(m, ref_wp, ratio, ego_x, ego_y, ego_s, ego_d, ego_lane, nwp_unused)) {
-        ego_s = ego_d = 0;
-        ego_lane = 0;
-        status |= PP_ST_EGO_UNMATCHED;
-    }
-    double ego_vs, ego_vd;
-    project_speed(m, esv_x, esv_y, ref_wp, ego_vs, ego_vd);
-    if (ego_acc > P.maximum_acc) ego_acc = P.maximum_acc;
-    if (ego_acc < -P.maximum_acc) ego_acc = -P.maximum_acc;
-
-    // ---- one streaming pass over the cars in ascending id (std::map order) ----
-    // LaneChangePlanner accumulation (src/main.cpp:377-445) and follow-car selection
-    // (src/main.cpp:1388-1410) are order-dependent reductions over the same car sequence.
+    EgoSt e;
+    prep_ego<1>(m, in, P, S, s, 0, e);
+    uint32_t status = e.status;
     const int T_in = in.prev_target_lane[s];
-    int lane_speed[NL];                     // the int-truncated lane speed where bit l of ls_set
-    int ls_set = 0;                         // (else P.max_speed)
-    double next_s[NL];
-    bool open[NL];
-    int in_id = -1; double in_s = 0;
-    int t_id[NL];
-    double t_s[NL];
-#pragma unroll
-    for (int l = 0; l < NL; l++) {
-        lane_speed[l] = 0; next_s[l] = 1000; open[l] = true;
-        t_id[l] = -1; t_s[l] = 0;
-    }
-    int nmatched = 0;
+    PlanAcc a;
+    a.init();
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
     // Without a car table: the frame's rows in order (ascending ids). With one (the reference's
@@ -234,14 +544,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
 #else
     const int iters = tab ? in.tab_slots : ncar;
 #endif
-    // Visiting order. Every per-car reduction below is a minimum with ties to the lower iteration
-    // index (or an AND / a count), so any visiting order gives the reference's result once ties
-    // compare that index explicitly. Without a car table the rows are visited nearest first
-    // (squared distance to the ego, a 4-bit row index in the low mantissa bits of a float key,
-    // sorted by a Batcher network): the k-th visit of every lane of a wave then walks a similar
-    // number of lane segments in lane_matching, which is where the divergence was. With a table,
-    // or a negative car id (the reference's -1 'no car' sentinel), the identity order is kept.
-    // (more than 16 rows: the identity order)
+    // Visiting order (PlanAcc: any order once ties compare the iteration index). Without a car
+    // table the rows are visited nearest first (squared distance to the ego, a 4-bit row index in
+    // the low mantissa bits of a float key, sorted by a Batcher network): the k-th visit of every
+    // lane of a wave then walks a similar number of lane segments in lane_matching, which is where
+    // the divergence was. With a table, or a negative car id (the reference's -1 'no car'
+    // sentinel), the identity order is kept. (more than 16 rows: the identity order)
     uint64_t order = 0xFEDCBA9876543210ull;
     bool sorted = false;
 #if PP_CAR_SORT
@@ -253,9 +561,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             key[j] = 0xFFFFFFF0u | (uint32_t)j;
             if (j < iters) {
                 const int64_t ix = (int64_t)j * S + s;
-                const double dx = in.car_x[ix] - ego_x, dy = in.car_y[ix] - ego_y;
+                const double dx = in.car_x[ix] - e.ego_x, dy = in.car_y[ix] - e.ego_y;
                 const float f = (float)(dx * dx + dy * dy);
+#if PP_CAR_SORT_BATCH
+                // rows in batches of PP_CAR_SORT_BATCH, nearest first inside a batch: the rows a
+                // wave gathers from stay few while a batch is visited (L2 locality)
+                key[j] = ((uint32_t)(j / PP_CAR_SORT_BATCH) << 28) | ((__float_as_uint(f) >> 3) & 0x0FFFFFF0u) | (uint32_t)j;
+#else
                 key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
+#endif
                 neg |= in.car_id[ix] < 0;
             }
         }
@@ -280,13 +594,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
         }
     }
 #endif
-    // iteration index of each running minimum, 6 bits each: next_s[l] at field l, the target-lane
-    // car of lane l at field NL + l, the in-lane car at field 2 NL (the follow cars' velocities are
-    // re-read from that index after the pass)
     static_assert((2 * NL + 1) * 6 <= 64 && PP_MAX_CARS <= 64, "iteration index fields");
-    uint64_t its = 0;
-    auto it_of = [&](int f) { return (int)((its >> (6 * f)) & 63); };
-    auto set_it = [&](int f, int it) { its = (its & ~(63ull << (6 * f))) | ((uint64_t)it << (6 * f)); };
     int p = 0;                              // next unread row (table mode)
     for (int kk = 0; kk < iters; kk++) {
         const int it = sorted ? (int)((order >> (4 * kk)) & 15) : kk;
@@ -305,23 +613,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             const int64_t ix = (int64_t)row * S + s;
             id = in.car_id[ix];
             cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
-            if (draw > 0) {                     // Monte-Carlo sensor noise (include/pp.h pp_params)
-                const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
-                cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 0);
-                cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 1);
-                cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 2);
-                cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
-            }
+            if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
             int nwp = 0;
 #ifdef PP_ABL_SKIP_FAR   // diagnostic timing build: cars beyond PP_ABL_SKIP_FAR metres skipped
-            if ((cx - ego_x) * (cx - ego_x) + (cy - ego_y) * (cy - ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
+            if ((cx - e.ego_x) * (cx - e.ego_x) + (cy - e.ego_y) * (cy - e.ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
 #endif
             PP_DIAGC(17, true);
 #ifdef PP_ABL_NO_MATCH     // diagnostic timing build: no lane matching of the cars
-            cs = ego_s + (cx - ego_x); cd = 6.0 + 0.1 * (cy - ego_y); clane = 1; nwp = ref_wp;
+            cs = e.ego_s + (cx - e.ego_x); cd = 6.0 + 0.1 * (cy - e.ego_y); clane = 1; nwp = e.ref_wp;
             if (false) {
 #else
-            if (!lane_match(m, ref_wp, ratio, cx, cy, cs, cd, clane, nwp)) {
+            if (!lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
 #endif
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;
@@ -338,183 +640,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
             id = sid;
             clane = in.tab_lane[tix];
             cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
-            cvx = in.tab_vx[tix]; cvy = in.tab_vy[tix];
         }
-        nmatched++;
-        // planner (src/main.cpp:379-444)
-        const double sp = cs + cvs * dt0;
-        if (sp > ego_s) {
-            // the first car (in iteration order) with the smallest sp sets next_s; lane_speed
-            // comes from it if it is within 200 m (an earlier, larger minimum never is then)
-            // (next_s == 1000: still the initial value, which no car can set, so it wins the tie)
-            if (sp < next_s[clane] || (sp == next_s[clane] && next_s[clane] != 1000 && it < it_of(clane))) {
-                next_s[clane] = sp;
-                set_it(clane, it);
-                if (sp - ego_s < 200) {
-                    int speed = (int)cvs;
-                    if (speed > P.max_speed) speed = (int)P.max_speed;
-                    if (sp - ego_s > 100)
-                        speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
-                    lane_speed[clane] = speed;
-                    ls_set |= 1 << clane;
-                } else {
-                    ls_set &= ~(1 << clane);
-                }
-            }
-        }
-        double add = 2;
-        if (T_in == clane) add = 0;
-        const double min_dist = P.car_length + P.safety_distance + add;
-        if (fabs(ego_s - sp) < min_dist) open[clane] = false;
-        if (sp > ego_s && cvs < ego_vs) {
-            const double car_dist = sp - ego_s - P.car_length - P.safety_distance - add;
-            const double sd = ego_vs - cvs;
-            const double dtm = sd / P.relaxed_acc;
-            const double ddist = ego_vs * dtm - sd / 2 * dtm;
-            if (car_dist < ddist) open[clane] = false;
-        }
-        if (sp < ego_s && cvs > ego_vs && sp + 50 > ego_s) {
-            const double car_dist = ego_s - sp - P.car_length - P.safety_distance - add;
-            const double sd = cvs - ego_vs;
-            double dtm = sd / P.relaxed_acc;
-            if (T_in == ego_lane) dtm += 2;
-            const double md = sd * dtm;
-            if (car_dist < md) open[clane] = false;
-        }
-        // follow cars (src/main.cpp:1391-1409); the target-lane choice for every candidate lane
-        const double s0 = cs + cvs * dt0;
-        const double d0 = cd + cvd * dt0;
-        if (s0 > ego_s && fabs(d0 - ego_d) < 3) {
-            if (in_id == -1 || in_s > s0 || (in_s == s0 && it < it_of(2 * NL))) {
-                in_id = id; in_s = s0; set_it(2 * NL, it);
-            }
-        }
-#pragma unroll
-        for (int L = 0; L < NL; L++) {
-            if (s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3) {
-                if (t_id[L] == -1 || t_s[L] > s0 || (t_s[L] == s0 && it < it_of(NL + L))) {
-                    t_id[L] = id; t_s[L] = s0; set_it(NL + L, it);
-                }
-            }
-        }
+        a.add(P, e, T_in, it, id, cs, cd, clane, cvs, cvd);
     }
-    // scores + argmax (src/main.cpp:447-484)
-    int best_lane = ego_lane;
-    double best_score = 0;
-    double score[NL];
-#pragma unroll
-    for (int lane = 0; lane < NL; lane++) {
-        score[lane] = 0;
-        if (lane != ego_lane && !open[lane]) continue;
-        const double lsp = ((ls_set >> lane) & 1) ? (double)lane_speed[lane] : P.max_speed;
-        const double speed_score = s_min(lsp / P.max_speed, 1.0);
-        const double distance_score = 1 - fabs((double)(T_in - lane)) / 2;
-        const double free_score = s_min(1.0, next_s[lane] / 100);
-        const double total = speed_score + distance_score / 2 + free_score;
-        score[lane] = total;
-        if (total > best_score) { best_score = total; best_lane = lane; }
-    }
-    int T;
-    if (abs(ego_lane - best_lane) > 1) {
-        const int nl = best_lane > ego_lane ? ego_lane + 1 : ego_lane - 1;
-        T = open[nl] ? nl : ego_lane;
-        status |= PP_ST_JUMP_RULE;
-    } else {
-        T = best_lane;
-    }
-    int open_mask = 0;
-#pragma unroll
-    for (int l = 0; l < NL; l++) open_mask |= open[l] ? (1 << l) : 0;
-    if (open_mask != (1 << NL) - 1) status |= PP_ST_LANE_CLOSED;
-    if (T != ego_lane) {                                               // src/main.cpp:1358-1369
-        const double dtl = lane_offset(T);
-        const double diff = fabs(ego_vd * 1.0 + ego_d - dtl);
-        if (diff > 6.0) { T = ego_lane; status |= PP_ST_TOO_FAR; }
-    }
-    // LimitSpeed for the in-lane car and the per-lane target car (src/main.cpp:1411-1438)
-    int lim_mask = 0;
-    bool col;
-    // the reference's "no car" is id -1 (src/main.cpp:1383-1432): a chosen car whose id is -1
-    // reads as none; ids are what :1411 compares
-    if (in_id != -1) {
-        double ts, tt;
-        double in_vx, in_vy;
-        car_velocity(in, P, S, s, draw, tab, it_of(2 * NL), in_vx, in_vy);
-        const int code = limit_speed(P, in_vx, in_vy, in_s, ego_s, ego_speed, ego_acc, true, ts, tt, col);
-        status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
-        pv.in_ts[v] = ts; pv.in_tt[v] = tt;
-        lim_mask |= 1;
-    }
-#pragma unroll
-    for (int L = 0; L < NL; L++) {
-        if (t_id[L] != -1 && t_id[L] != in_id) {
-            double ts, tt;
-            double t_vx, t_vy;
-            car_velocity(in, P, S, s, draw, tab, it_of(NL + L), t_vx, t_vy);
-            const int code = limit_speed(P, t_vx, t_vy, t_s[L], ego_s, ego_speed, ego_acc, false, ts, tt, col);
-            status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
-            pv.l_ts[L * Sv + v] = ts; pv.l_tt[L * Sv + v] = tt;
-            lim_mask |= 2 << L;
-        }
-    }
-    // TrajectoryBuilder::build start pose (src/main.cpp:583-610) + frame rotations (:786-823)
-    double pos_x, pos_y, angle;
-    if (K == 0) {
-        pos_x = ego_x; pos_y = ego_y;
-        angle = yaw * kPi / 180;
-    } else {
-        pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
-        const double vx = pos_x - p8x, vy = pos_y - p8y;
-        if (vx * vx + vy * vy < kEps) angle = yaw * kPi / 180;
-        else angle = ppg::atan2(pos_y - p8y, pos_x - p8x);      // glibc's atan2, bit for bit
-    }
-    // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
-    // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
-    if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
-    {   // k_cand<false> divides by reciprocals without range checks: speeds and ramp times in range
-        bool ok = speed_in_range(ego_speed);
-        for (int k = 0; k < P.n_speeds; k++) {
-            const double vk = cand_speed(P, ego_speed, k);
-            ok = ok && speed_in_range(vk) && speed_in_range(fabs(ego_speed - vk) / P.relaxed_acc);
-        }
-        if (lim_mask & 1) ok = ok && speed_in_range(pv.in_ts[v]) && speed_in_range(pv.in_tt[v]);
-#pragma unroll
-        for (int L = 0; L < NL; L++)
-            if (lim_mask & (2 << L)) ok = ok && speed_in_range(pv.l_ts[L * Sv + v]) && speed_in_range(pv.l_tt[L * Sv + v]);
-        if (!ok) lim_mask |= kLimSlow;
-    }
-    if (lim_mask & kLimSlow) {
-        const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
-        for (int b = 0; b < gb.BPS; b++) atomicOr(&gb.bits[(g0 + b) >> 5], 1u << ((g0 + b) & 31));
-    }
-    pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
-    // the frame's rotations cos(-angle), sin(-angle) (:786-787) and cos(angle), sin(angle)
-    // (:822-823) as the reference's libm computes them (pp_glibcm.h): every knot is a product with
-    // them, so the spline and every path position carry their exact bits. Headings of 1e8 rad and
-    // more (only from an absurd telemetry yaw) are outside the restated reduction.
-    double cm, sm, cp, sp_;
-    if (!(ppg::cos(-angle, cm) && ppg::sin(-angle, sm) && ppg::cos(angle, cp) && ppg::sin(angle, sp_))) {
-        ppm::sincos_pp<true>(-angle, sm, cm);
-        ppm::sincos_pp<true>(angle, sp_, cp);
-    }
-    pv.ca_m[v] = cm; pv.sa_m[v] = sm;
-    pv.ca_p[v] = cp; pv.sa_p[v] = sp_;
-    pv.ego_speed[v] = ego_speed; pv.ego_d[v] = ego_d; pv.ego_vd[v] = ego_vd;
-#pragma unroll
-    for (int l = 0; l < NL; l++) { pv.ratio[l * Sv + v] = ratio[l]; pv.score[l * Sv + v] = score[l]; }
-    pv.K[v] = K; pv.ref_wp[v] = ref_wp; pv.T[v] = T; pv.ego_lane[v] = ego_lane;
-    pv.open_mask[v] = open_mask; pv.lim_mask[v] = lim_mask; pv.status[v] = status;
-    if (draw == 0) out_status[s] = 0;        // k_cand ORs its flags in (atomics when a scene spans blocks)
-    if (info && draw == 0) {
-        pp_scene_info I = {};
-        I.ego_x = ego_x; I.ego_y = ego_y; I.ego_speed = ego_speed; I.ego_acc = ego_acc;
-        I.ego_s = ego_s; I.ego_d = ego_d; I.ego_vs = ego_vs; I.ego_vd = ego_vd;
-        for (int l = 0; l < NL; l++) { I.ref_ratio[l] = ratio[l]; I.lane_score[l] = score[l]; }
-        I.ref_wp = ref_wp; I.ego_lane = ego_lane; I.target_lane = T; I.lane_open_mask = open_mask;
-        I.n_matched_cars = nmatched; I.in_lane_car = in_id;
-        info[s] = I;
-    }
+    prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
 }
+
+// K1 for small batches: a group of G lanes per evaluation (G = 2 ... 16; kernels k_prep_g2 ... k_prep_g16), so that a batch of a few
+// thousand scenes still fills the chip (BASELINE config 2: 4,096 scenes). Lane r of a group matches
+// rows r, r + G, ... (coalesced across the group) and scans every G-th waypoint for the Frenet
+// frame; the planner's pass then runs over each round's G cars in ascending row order on every
+// lane of the group (the cars' Frenet states exchanged by lane shuffles), i.e. in the reference's
+// own iteration order. No car table (pp_eval picks k_prep for table mode).
+template <bool kLdsMap, int G>
+__device__ __forceinline__ void prep_grp_body(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+                                              pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
+    static_assert(G >= 2 && G <= 16 && (G & (G - 1)) == 0, "group: a power of two in [2, 16]");
+    extern __shared__ __attribute__((aligned(16))) double smap[];
+    const int n = mg.n;
+    if (kLdsMap) {
+        for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
+        __syncthreads();
+    }
+    const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
+    const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
+    const int r = (int)(threadIdx.x % G);
+    const int64_t v = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
+    if (v >= Sv) return;                      // whole groups leave together
+    const int64_t s = D == 1 ? v : v / D;
+    const int draw = (int)(v - s * D);
+
+    EgoSt e;
+    prep_ego<G>(m, in, P, S, s, r, e);
+    uint32_t status = e.status;
+    const int T_in = in.prev_target_lane[s];
+    PlanAcc a;
+    a.init();
+    int ncar = in.n_cars[s];
+    if (ncar > in.car_stride) ncar = in.car_stride;
+    uint32_t ust = 0;
+    for (int j0 = 0; j0 < ncar; j0 += G) {
+        const int j = j0 + r;
+        int okl = 0, id = 0;                  // okl: matched | lane << 1
+        double cs = 0, cd = 0, cvs = 0, cvd = 0;
+        if (j < ncar) {
+            const int64_t ix = (int64_t)j * S + s;
+            id = in.car_id[ix];
+            double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+            if (draw > 0) car_noise(P, s, draw, j, cx, cy, cvx, cvy);
+            int nwp = 0, clane = 0;
+            if (lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
+                project_speed(m, cvx, cvy, nwp, cvs, cvd);
+                okl = 1 | (clane << 1);
+            } else {
+                ust |= PP_ST_CAR_UNMATCHED;
+            }
+        }
+        const int nq = ncar - j0 < G ? ncar - j0 : G;
+        for (int q = 0; q < nq; q++) {
+            const int qokl = __shfl(okl, q, G);
+            const int qid = __shfl(id, q, G);
+            const double qcs = __shfl(cs, q, G), qcd = __shfl(cd, q, G);
+            const double qcvs = __shfl(cvs, q, G), qcvd = __shfl(cvd, q, G);
+            if (qokl & 1) a.add(P, e, T_in, j0 + q, qid, qcs, qcd, qokl >> 1, qcvs, qcvd);
+        }
+    }
+    status |= grp_or<G>(ust);
+    prep_finish<G>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, false, r, T_in, e, a, status);
+}
+
+// the grouped instantiations by name (pp_eval's launch switch)
+#define PP_PREP_GRP(NAME, G)                                                                         \
+    template <bool kLdsMap>                                                                         \
+    __global__ __launch_bounds__(256) void NAME(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,  \
+                                                pp_scene_info* info, uint32_t* os, GroupBits gb) {   \
+        prep_grp_body<kLdsMap, G>(mg, in, P, pv, info, os, gb);                                     \
+    }
+PP_PREP_GRP(k_prep_g2, 2)
+PP_PREP_GRP(k_prep_g4, 4)
+PP_PREP_GRP(k_prep_g8, 8)
+PP_PREP_GRP(k_prep_g16, 16)
+#undef PP_PREP_GRP
 
 // ------------------------------------------------------------------------------------------------
 // Phase A: control points + spline for one (scene, lane) into a slot
@@ -902,10 +1110,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (kOutMode != 0 && kOut) {
                 const double tx = pos_x * ca - pos_y * sa;
                 const double ty = pos_x * sa + pos_y * ca;
-                if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-                if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+                if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
             }
-            if (kOutMode == 3 && kRec) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
+            if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
             ng++;
             R.travelled += dstep;
         }
@@ -1120,7 +1328,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     double nad = kLarge ? nc / speed / 50
                                         : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
-                    rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
+                    if (PP_CHKP(rec + 2 * rstride + ng * ws, rec, nrec, 6))
+                        rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
                     R.adj[ng >> 6] |= 1ull << (ng & 63);
                 }
                 eff_c = nc;
@@ -1159,10 +1368,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         if (kOutMode != 0 && kOut) {
             const double tx = pos_x * ca - pos_y * sa;
             const double ty = pos_x * sa + pos_y * ca;
-            if (wx) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-            if (px) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+            if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
         }
-        if (kOutMode == 3 && kRec) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
+        if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -1251,6 +1460,10 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     // the range of the unchecked divisions) -> the scene runs in the k_cand<true> instantiation
     uint32_t* sSlow = sFlags + SPB;
     if (tid < SPB) { sFlags[tid] = 0; sSlow[tid] = 0; }
+#ifdef PP_CHECK
+    for (int i = tid; i < 5 * nslot * kKP; i += (int)blockDim.x) sX[i] = __builtin_nan("");
+    for (int i = tid; i < 4 * nslot; i += (int)blockDim.x) sMeta[i] = kMetaPoison;
+#endif
     __syncthreads();
     bool mine = false;
     for (int t = tid; t < nsc * D; t += (int)blockDim.x) {
@@ -1342,6 +1555,13 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         const int L = cc / NS, k = cc - L * NS;
         const int j = sc_l * NL + L;
         const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
+#ifdef PP_CHECK
+        {   // the slot was written by this group's phase A (not left over from an earlier group)
+            const int nk_ = sl.m(0), ncp_ = sl.m(1), npk_ = sl.m(2);
+            chk_(j < nslot && nk_ != kMetaPoison && nk_ >= 1 && nk_ <= kKP && ncp_ >= 1 && ncp_ <= 6 &&
+                 npk_ >= 0 && npk_ < PP_PREV_KEEP, 20, j, g);
+        }
+#endif
         const double vt = cand_speed(P, pv.ego_speed[v], k);
         const SC sc = make_sc(P, pv, Sv, v, L, vt);
         const int K = pv.K[v], T = pv.T[v];
@@ -1356,6 +1576,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             double* wy = nullptr;
             if (winner) {
                 for (int i = 0; i < K; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 9)) break;
                     out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
                     out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
                 }
@@ -1365,6 +1586,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             const int64_t ps = (int64_t)C * 2;
             double* p0 = out.paths + ((s * N) * C + c) * 2;
             for (int i = 0; i < K; i++) {
+                if (!PP_CHKP(p0 + i * ps + 1, paths, npaths, 7)) break;
                 p0[i * ps] = in.prev_x[(int64_t)i * S + s];
                 p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
             }
@@ -1372,10 +1594,16 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
                                                        pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
                                                        px, ps);
-            for (int i = R.ng; i < N - K; i++) { px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan(""); }
-            if (out.path_len) out.path_len[s * C + c] = K + R.ng;
+            for (int i = R.ng; i < N - K; i++) {
+                if (!PP_CHKP(px + i * ps + 1, paths, npaths, 8)) break;
+                px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan("");
+            }
+            if (out.path_len && PP_CHK(s * C + c < g_lim.ncost, 11, s * C + c)) out.path_len[s * C + c] = K + R.ng;
             if (winner) {
-                for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
+                for (int i = K + R.ng; i < N; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 10)) break;
+                    out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0;
+                }
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
             }
@@ -1388,7 +1616,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
             R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
                                                        S, nullptr, 0, winner, rec + s);
-            if (winner) {
+            if (winner && PP_CHK(s < g_lim.nscen, 12, s) && PP_CHKP(adjm + S + s, adjm, nadj, 13)) {
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
                 adjm[s] = R.adj[0];
@@ -1402,13 +1630,14 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * Sv + v], L, T, vt, pv.open_mask[v],
                                       pv.ego_lane[v], flags);
-        out.cost[s * C + c] = cost;
+        if (PP_CHKP(out.cost + s * C + c, cost, ncost, 14)) out.cost[s * C + c] = cost;
         if (D > 1) flags |= (uint32_t)pv.status[v];     // every draw's planner flags
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
     if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
         const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
+        if (!PP_CHK(s0 + tid < g_lim.nscen, 15, s0 + tid)) return;
         if (BPS == 1) out.status[s0 + tid] = st;
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
     }
@@ -1556,6 +1785,10 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
             const int g = g0 + u;
             const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
             bits |= bit ? 1u << u : 0u;
+#ifdef PP_CHECK
+            if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 16); }
+            if (bit) { PP_CHKP(rec + 2 * rstride + (int64_t)g * S + s, rec, nrec, 16); }
+#endif
             px_[u] = g < ng ? rec[(int64_t)g * S + s] : 0.0;
             py_[u] = g < ng ? rec[rstride + (int64_t)g * S + s] : 0.0;
             rt[u] = bit ? rec[2 * rstride + (int64_t)g * S + s] : 0.0;
@@ -1590,6 +1823,7 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
             }
             const double tx = px_[u] * ca - py_[u] * sa;
             const double ty = px_[u] * sa + py_[u] * ca;
+            if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
             out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
             out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
             pxp = px_[u];
@@ -2005,6 +2239,27 @@ PrepV prep_bind(void* base, int64_t S) {
     return p;
 }
 
+// K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
+// SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. pp_set_prep_group (or
+// the PP_PREP_G environment variable) forces a value.
+std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
+bool prep_group_ok(int G) { return G == 0 || G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
+int prep_group(int64_t Sv) {
+    int forced = g_prep_forced.load(std::memory_order_relaxed);
+    if (forced < 0) {
+        const char* e = getenv("PP_PREP_G");
+        forced = e && prep_group_ok(atoi(e)) ? atoi(e) : 0;
+        int expect = -1;
+        g_prep_forced.compare_exchange_strong(expect, forced);
+        forced = g_prep_forced.load(std::memory_order_relaxed);
+    }
+    if (forced > 0) return forced;
+    const int64_t target = 256LL * 4 * 64 * 2;
+    int G = 1;
+    while (G < 16 && Sv * G * 2 <= target) G *= 2;
+    return G;
+}
+
 int cands_per_block(int C) {
     int spb = 256 / C;
     if (spb > 64 / NL) spb = 64 / NL;      // <= 64 LDS spline slots per workgroup
@@ -2108,6 +2363,17 @@ double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int3
     return ppsynth::mc_gauss(seed, (uint64_t)scene, draw, car, q);
 }
 
+#ifdef PP_CHECK
+int32_t pp_check_read(unsigned long long* out, int32_t reset) {  // checking builds only: g_chk[8]
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 #ifdef PP_DIAG
 int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic builds only
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
@@ -2309,17 +2575,42 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
-    // K1
+#ifdef PP_CHECK
+    {   // checking builds: the bounds of every buffer this call's kernels store into
+        ChkLim L = {};
+        const long long Cn = (long long)Dn * NL * P.n_speeds;
+        L.paths = R.paths; L.npaths = R.paths ? (long long)S * P.n_points * Cn * 2 : 0;
+        L.nx = R.next_x; L.ny = R.next_y; L.nnext = (long long)S * P.n_points;
+        L.rec = rec; L.nrec = rec ? 3LL * PP_MAX_POINTS * W.rec_cap : 0;
+        L.adjm = (const unsigned long long*)adjm; L.nadj = adjm ? 2LL * W.rec_cap : 0;
+        L.cost = R.cost; L.ncost = (long long)S * Cn; L.nscen = S;
+        if (hipStreamSynchronize(st) != hipSuccess ||
+            hipMemcpyToSymbol(HIP_SYMBOL(g_lim), &L, sizeof L) != hipSuccess) return PP_ERR_HIP;
+    }
+#endif
+    // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
         const int threads = 256;
-        const int64_t blocks = (Sv + threads - 1) / threads;
+        const int G = B.tab_valid ? 1 : prep_group(Sv);
+        const int64_t blocks = (Sv * G + threads - 1) / threads;
         if (timing) (void)hipEventRecord(ev[0], st);
-        if (mg.n <= kLdsMapMax) {
-            const size_t lds = sizeof(double) * kMapArrays * (size_t)mg.n;
-            hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb);
-        } else {
-            hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb);
+#ifdef PP_PREP_GMAP   // diagnostic timing build: k_prep reads the map through L1/L2 at any size
+        const bool lmap = false;
+#else
+        const bool lmap = mg.n <= kLdsMapMax;
+#endif
+        const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
+#define PP_LAUNCH_PREP(KER) \
+        if (lmap) hipLaunchKernelGGL(KER<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb); \
+        else hipLaunchKernelGGL(KER<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb)
+        switch (G) {
+            case 2: { PP_LAUNCH_PREP(k_prep_g2); break; }
+            case 4: { PP_LAUNCH_PREP(k_prep_g4); break; }
+            case 8: { PP_LAUNCH_PREP(k_prep_g8); break; }
+            case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
+            default: { PP_LAUNCH_PREP(k_prep); break; }
         }
+#undef PP_LAUNCH_PREP
     }
     // K2: the full grid for the scenes in the proven range, then the flagged groups only
     {
@@ -2351,6 +2642,12 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     }
     if (timing) (void)hipEventRecord(ev[3], st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+    return PP_OK;
+}
+
+int32_t pp_set_prep_group(int32_t lanes) {
+    if (!prep_group_ok(lanes)) return PP_ERR_ARG;
+    g_prep_forced.store(lanes, std::memory_order_relaxed);
     return PP_OK;
 }
 

@@ -134,7 +134,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
            "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device",
-           "pp_num_lanes", "pp_libm_eval"]
+           "pp_num_lanes", "pp_libm_eval", "pp_set_prep_group"]
 
 
 def _load():
@@ -167,6 +167,8 @@ def _load():
                                   C.c_double, _dp, _dp, C.c_int32, _ip, _dp, _dp, _dp, _dp,
                                   C.c_int32, _ip, _dp, _dp, _ip]
     lib.pp_plan_frame.restype = C.c_int32
+    lib.pp_set_prep_group.argtypes = [C.c_int32]
+    lib.pp_set_prep_group.restype = C.c_int32
     lib.pp_timing_enable.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     lib.pp_timing_enable.restype = C.c_int32
     lib.pp_timing_read.argtypes = [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64)]
@@ -540,6 +542,11 @@ def plan_frame(m: Map, ego_x, ego_y, ego_yaw_deg, ego_speed_mph, prev_x, prev_y,
 
 
 DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
+
+
+def set_prep_group(lanes):
+    """K1 lanes per evaluation (1, 2, 4, 8, 16; 0 = automatic): pp_set_prep_group."""
+    _check(lib.pp_set_prep_group(lanes), "pp_set_prep_group")
 
 
 def highway_map():

@@ -363,6 +363,10 @@ int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
  * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the
  * summed milliseconds and launch counts per kernel, and clears the record. */
+/* Tuning: lanes per evaluation of the scene-preparation kernel (K1): 1, 2, 4, 8 or 16; 0 = automatic
+ * (more lanes per scene when a batch is too small to fill the device). Results do not depend on it.
+ * Process-wide; returns PP_ERR_ARG for other values. */
+int32_t pp_set_prep_group(int32_t lanes);
 int32_t pp_timing_enable(pp_map* m, int32_t device, int32_t enable);
 int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches3);
 

@@ -29,3 +29,26 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Checking builds (-DPP_CHECK, tools/variants.sh check): after the GPU tests, read the
+    kernels' bounds/LDS-poison violation record (pp_check_read) into $PP_CHECK_OUT; any violation
+    fails the session."""
+    out = os.environ.get("PP_CHECK_OUT")
+    if not out or not gpu_available():
+        return
+    import ctypes as C
+    import json
+    import ppamd
+    lib = C.CDLL(ppamd.LIB_PATH)
+    if not hasattr(lib, "pp_check_read"):      # not a checking build (e.g. a child's 4-lane library)
+        return
+    buf = (C.c_ulonglong * 8)()
+    rc = lib.pp_check_read(buf, 0)
+    rec = {"lib": os.path.basename(ppamd.LIB_PATH), "rc": rc, "violations": buf[0],
+           "first_site": buf[1], "first_offset": buf[2], "first_block": buf[3], "first_group": buf[4]}
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    if rc != 0 or buf[0] != 0:
+        session.exitstatus = 1

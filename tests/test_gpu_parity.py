@@ -263,3 +263,47 @@ def test_full_size_properties(env):
     got = {k: (v[:, idx] if k.startswith("next") else v[idx])
            for k, v in ppamd.result_to_numpy({k: r1[k] for k in ("winner", "n_out", "next_x", "next_y", "cost", "status")}).items()}
     compare(got, ref)
+
+
+@pytest.mark.parametrize("case", ["random", "ties_ids", "rows24", "draws"])
+def test_prep_group_invariance(env, case):
+    """K1 runs one lane per evaluation on large batches (cars nearest first) and a group of G lanes
+    per evaluation on small ones (rows split over the group, planner in row order): every G
+    (pp_set_prep_group) gives bit-identical outputs, and G = 1 and G = 16 equal the oracle. Cases:
+    random scenes; tied duplicate cars with -1, negative and large ids; 24 rows (more than one
+    round per group); Monte-Carlo draws (one group per scene x draw)."""
+    import test_cartable
+    S = 900
+    kw = {"emit_paths": True}
+    if case == "rows24":
+        sc = test_cartable.many_car_scenes(env["m"], S, 4321, test_cartable.ids_wide)
+    else:
+        sc = ppamd.synth_host(env["m"], S, seed=31, first=777)
+    if case == "ties_ids":
+        for j in range(6, 12):
+            for k in ("car_x", "car_y", "car_vx", "car_vy"):
+                sc[k][j, ::2] = sc[k][j - 6, ::2]
+        sc["car_id"][:, 1::4] = (np.arange(12) * 1000 + 1000)[:, None]
+        sc["car_id"][0, 3::4] = -1
+    if case == "draws":
+        kw = {"n_speeds": 1, "n_draws": 8, "noise_seed": 5}
+    prm = ppamd.default_params(**kw)
+    d = to_dev(env, sc)
+    outs = {}
+    try:
+        for g in (1, 2, 4, 8, 16):
+            ppamd.set_prep_group(g)
+            outs[g] = run_gpu(env, d, prm, info=case != "draws")
+    finally:
+        ppamd.set_prep_group(0)
+    def same(a, b):
+        if a.dtype.names:
+            return all(same(a[f], b[f]) for f in a.dtype.names)
+        return np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+    for g in (2, 4, 8, 16):
+        for k, v in outs[1].items():
+            assert same(outs[g][k], v), (g, k)
+    if case != "draws":
+        ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+        compare(outs[1], ref)
+        compare(outs[16], ref)
