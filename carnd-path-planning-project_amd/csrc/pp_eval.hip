@@ -1051,7 +1051,8 @@ __device__ void team_a5(const Slot& sl, int r, int TS) {
 // ------------------------------------------------------------------------------------------------
 // Phase B: the resampling loop of one candidate (src/main.cpp:845-1041)
 // ------------------------------------------------------------------------------------------------
-struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj[2]; };
+// adj0/adj1: the adjusted steps 0-63 / 64-127 (two registers: an indexed pair would live in scratch)
+struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj0, adj1; };
 
 // Output modes. The curvature adjustment (src/main.cpp:972-1018) rotates only the local->global
 // transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that the cost reads
@@ -1074,7 +1075,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     const bool kRec = kOutMode == 3 && out_on;
     const int64_t rstride = (int64_t)room * ws;
     CandRes R;
-    R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0; R.adj[0] = 0; R.adj[1] = 0;
+    R.acc_sum = 0; R.travelled = 0; R.ng = 0; R.flags = 0; R.adj0 = 0; R.adj1 = 0;
     const int nk = sl.m(0), ncp = sl.m(1), npk = sl.m(2), mflags = sl.m(3);
     if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
@@ -1303,7 +1304,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 double nc = P.maximum_acc - acc;
                 if (nc < 0) nc = 0;
                 if (kOutMode != 0 && kOut) {
-                    double nad = nc / speed / 50;
+                    // the transform's turn about the current point (src/main.cpp:986-997); the frame's
+                    // new cos/sin by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead
+                    // of sin/cos of the accumulated angle (~1 ulp per adjustment, as k_emit; DESIGN.md
+                    // §5); rot by reciprocal divisions in k_cand<false> (as the recorded rot, below)
+                    double nad = kLarge ? nc / speed / 50
+                                        : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
                     const double rot = nad - adiff;
                     double tpx = pos_x * ca - pos_y * sa;
@@ -1318,7 +1324,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     cx = tpx + rvx;
                     cy = tpy + rvy;
                     tangle += rot;
-                    ppm::sincos_pp<kLarge>(tangle, sa, ca);
+                    const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
+                    ca = nca; sa = nsa;
                 }
                 if (kOutMode == 3 && kRec) {
                     // rot only turns the output transform (k_emit), so it need not carry the
@@ -1330,7 +1337,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     if (adiff < 0) nad *= -1;
                     if (PP_CHKP(rec + 2 * rstride + ng * ws, rec, nrec, 6))
                         rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
-                    R.adj[ng >> 6] |= 1ull << (ng & 63);
+                    const uint64_t bit = 1ull << (ng & 63);
+                    if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
                 }
                 eff_c = nc;
                 R.flags |= PP_ST_CURV_ADJUST;
@@ -1369,7 +1377,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const double tx = pos_x * ca - pos_y * sa;
             const double ty = pos_x * sa + pos_y * ca;
             if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-            if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+            if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
+                *(double2*)(px + ng * ps) = make_double2(tx + cx, ty + cy);     // one 16-B store (x, y)
         }
         if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
         ng++;
@@ -1619,8 +1628,8 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             if (winner && PP_CHK(s < g_lim.nscen, 12, s) && PP_CHKP(adjm + S + s, adjm, nadj, 13)) {
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
-                adjm[s] = R.adj[0];
-                adjm[S + s] = R.adj[1];
+                adjm[s] = R.adj0;
+                adjm[S + s] = R.adj1;
             }
         } else {
             R = run_candidate<kSlow, 0, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
@@ -1732,6 +1741,9 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
 // (src/main.cpp:994-1007), every point is mapped back with the current frame (:1033-1037). One lane
 // per scene; all loads/stores point-major (coalesced).
 // ------------------------------------------------------------------------------------------------
+// kChunk: recorded steps loaded together per lane (PP_EMIT_CHUNK for large batches; small batches,
+// where the kernel is one serial chain of memory round trips per lane, load 16 steps at a time)
+template <int kChunk>
 __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                               const double* rec, const uint64_t* adjm) {
     const int64_t S = in.n_scenes;
@@ -1766,7 +1778,7 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
     // A rotation beyond sincos_pp's medium range (a step that slowed to ~1e-7 m/s) sends the
     // lane's chunk through a per-step loop with the library reduction, re-reading the record:
     // the unrolled chunk then holds no call and stays register-light.
-    constexpr int kEmitChunk = PP_EMIT_CHUNK;
+    constexpr int kEmitChunk = kChunk;
     auto rotate = [&](double rot, double& cr, double& sr) {
         const double tpx = (pxp * ca - pyp * sa) + cx;
         const double tpy = (pxp * sa + pyp * ca) + cy;
@@ -2242,6 +2254,8 @@ PrepV prep_bind(void* base, int64_t S) {
 // K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
 // SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. pp_set_prep_group (or
 // the PP_PREP_G environment variable) forces a value.
+// k_emit: batches up to this many scenes take the small-batch instantiation
+constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
 bool prep_group_ok(int G) { return G == 0 || G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
 int prep_group(int64_t Sv) {
@@ -2631,8 +2645,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
     if (ref_direct && !P.emit_paths) {
-        const int64_t blocks = (S + 255) / 256;
-        hipLaunchKernelGGL(k_emit, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm);
+        if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
+            const int64_t blocks = (S + 63) / 64;
+            hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm);
+        } else {
+            const int64_t blocks = (S + 255) / 256;
+            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm);
+        }
     }
     // K3 (comfort mode, or any mode with draws): argmin + winner path
     if (!ref_direct) {
