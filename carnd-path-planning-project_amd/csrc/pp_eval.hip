@@ -1080,7 +1080,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
     double pos_x = 0, pos_y = 0;
-    double ca = ca0, sa = sa0, tangle = angle;
+    double ca = ca0, sa = sa0;
+    (void)angle;      // the frame turns by rotating (ca, sa) (src/main.cpp:996-997)
     double cur_t = 0.02;
     int ng = 0;
     if (mflags & kMetaFallback) {                                       // :848-901
@@ -1323,7 +1324,6 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     const double rvy = vx * sr + vy * cr;
                     cx = tpx + rvx;
                     cy = tpy + rvy;
-                    tangle += rot;
                     const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
                     ca = nca; sa = nsa;
                 }
@@ -1744,11 +1744,10 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
 // kChunk: recorded steps loaded together per lane (PP_EMIT_CHUNK for large batches; small batches,
 // where the kernel is one serial chain of memory round trips per lane, load 16 steps at a time)
 template <int kChunk>
-__global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
-                                              const double* rec, const uint64_t* adjm) {
+__device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_params& P, const PrepV& pv,
+                                           const pp_result& out, const double* rec, const uint64_t* adjm,
+                                           int64_t s) {
     const int64_t S = in.n_scenes;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
     const int N = P.n_points;
     const int K = pv.K[s];
     const int room = N - K;
@@ -1824,15 +1823,18 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
             }
             continue;
         }
+        // sin/cos of the chunk's turns first (rt = 0 where no turn): independent of each other and
+        // of the chain of turns below, so they overlap instead of queueing behind it
+        double crs[kEmitChunk], srs[kEmitChunk];
+        if (bits) {
+#pragma unroll
+            for (int u = 0; u < kEmitChunk; u++) ppm::sincos_pp<false>(rt[u], srs[u], crs[u]);
+        }
 #pragma unroll
         for (int u = 0; u < kEmitChunk; u++) {
             const int g = g0 + u;
             if (g >= ng) break;
-            if ((bits >> u) & 1) {
-                double cr, sr;
-                ppm::sincos_pp<false>(rt[u], sr, cr);
-                rotate(rt[u], cr, sr);
-            }
+            if ((bits >> u) & 1) rotate(rt[u], crs[u], srs[u]);
             const double tx = px_[u] * ca - py_[u] * sa;
             const double ty = px_[u] * sa + py_[u] * ca;
             if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
@@ -1872,6 +1874,37 @@ __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, Pr
     }
 #endif
     for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
+}
+
+template <int kChunk>
+__global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+                                              const double* rec, const uint64_t* adjm) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= in.n_scenes) return;
+    emit_scene<kChunk>(in, P, pv, out, rec, adjm, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// K2 + K4 in one launch for small batches in reference mode (no paths), where the step is a chain
+// of kernel latencies (BASELINE config 2: 4,096 scenes, ~1 wave per SIMD): the group's scenes in
+// the proven range (k_cand<false>'s code), then its flagged scenes (k_cand<true>'s code; the
+// group's bitmap bit is cleared as k_cand<true> clears it), then the lanes that recorded the
+// winners' paths (tid < nsc, kMode 1) replay the output transform from their own stores
+// (emit_scene). Two kernel boundaries fewer; waves_per_eu(1, 2): registers are not the limit here.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_cand_small(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm, uint32_t* gbits) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int64_t g = blockIdx.x;
+    cand_group<false, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+    __syncthreads();
+    if ((gbits[g >> 5] >> (g & 31)) & 1u) {                   // same word for every lane
+        cand_group<true, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+        if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
+    }
+    const int64_t s = g * SPB + threadIdx.x;
+    if ((int)threadIdx.x < SPB && s < in.n_scenes) emit_scene<16>(in, P, pv, out, rec, adjm, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2254,6 +2287,12 @@ PrepV prep_bind(void* base, int64_t S) {
 // K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
 // SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. pp_set_prep_group (or
 // the PP_PREP_G environment variable) forces a value.
+// k_cand_small (K2 + K4 in one launch) up to this many scenes; PP_FUSED=0/1 forces it off/on (A/B)
+constexpr int64_t kFusedSmall = 16384;
+bool fused_small(int64_t S) {
+    const char* e = getenv("PP_FUSED");
+    return e && *e ? atoi(e) != 0 : S <= kFusedSmall;
+}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
@@ -2544,6 +2583,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const bool ref_direct = prm->cost_mode == PP_COST_REFERENCE && Dn == 1;
     const CandGeom cg = cand_geom(Dn * NL * prm->n_speeds, S);
     if (cg.groups > 0x7fffffff) return PP_ERR_ARG;
+    // small batches in reference mode: K2 and K4 in one launch (k_cand_small)
+    const bool fused = ref_direct && !prm->emit_paths && cg.bps == 1 && fused_small(S);
     // the map lock is held from workspace binding through the (asynchronous) launches: a
     // concurrent call cannot grow and free this stream's buffers in between
     std::lock_guard<std::mutex> lk(M->mu);
@@ -2581,7 +2622,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             DS.ev_pool.pop_back();
             DS.ev_rec.push_back(ev[i]);
         }
-        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) ? 1 : 0);
+        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) && !fused ? 1 : 0);
     }
     pp_params P = *prm;
     pp_scene_batch B = *in;
@@ -2626,7 +2667,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         }
 #undef PP_LAUNCH_PREP
     }
-    // K2: the full grid for the scenes in the proven range, then the flagged groups only
+    // K2 (+ K4 for small batches in reference mode: k_cand_small)
     {
         const unsigned nb = (unsigned)cg.groups;
         const unsigned nslow = (unsigned)std::min<int64_t>(cg.groups, 2048);
@@ -2638,13 +2679,17 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
                            cg.spb, cg.bps, rec, adjm, W.gbits, ng)
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
+        else if (ref_direct && fused) {
+            hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
+                               cg.spb, rec, adjm, W.gbits);
+        }
         else if (ref_direct) { PP_LAUNCH_CAND(1); }
         else { PP_LAUNCH_CAND(0); }
 #undef PP_LAUNCH_CAND
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
-    if (ref_direct && !P.emit_paths) {
+    if (ref_direct && !P.emit_paths && !fused) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
             const int64_t blocks = (S + 63) / 64;
             hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm);

@@ -307,3 +307,28 @@ def test_prep_group_invariance(env, case):
         ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
         compare(outs[1], ref)
         compare(outs[16], ref)
+
+
+@pytest.mark.parametrize("case", ["random", "speed_edges"])
+def test_fused_small_invariance(env, case, monkeypatch):
+    """Small reference-mode batches run K2 and K4 in one launch (k_cand_small: the group's fast
+    scenes, its flagged scenes, then the winner lanes' output transform); PP_FUSED=0 forces the
+    three-launch path (k_cand<false>, k_cand<true>, k_emit). Both give bit-identical outputs and
+    equal the oracle. speed_edges: scenes flagged for the checked instantiation in most groups."""
+    S = 1200
+    sc = ppamd.synth_host(env["m"], S, seed=515, first=99)
+    if case == "speed_edges":
+        speeds = [-0.0, 5e-324, 1e-300, 1e-18, 0.3, 3e6, 1e300, -3.0]
+        for s in range(0, S, 3):
+            sc["n_prev"][s] = 0
+            sc["ego_speed_mph"][s] = speeds[(s // 3) % len(speeds)]
+    d = to_dev(env, sc)
+    prm = ppamd.default_params()
+    outs = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("PP_FUSED", f)
+        outs[f] = run_gpu(env, d, prm)
+    for k, v in outs["0"].items():
+        assert np.array_equal(outs["1"][k], v, equal_nan=v.dtype.kind == "f"), k
+    ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+    compare(outs["1"], ref)
