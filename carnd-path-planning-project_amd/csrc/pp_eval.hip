@@ -1426,6 +1426,68 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 #define PP_CAND_CACHE 1
 #endif
 
+// K4 inside k_cand (reference mode, emit_in): the winner lane of scene s replays the output
+// transform of its recorded path (src/main.cpp:994-1007, 1033-1037) with the sin/cos of each
+// recorded turn already in LDS (pcr/psr, one entry per step, computed by the block's team as
+// emit_scene computes them): only the chain of turns and points is left to the lane. Operations
+// and order are emit_scene's, so the outputs are bit-identical to the k_emit path.
+template <int kChunk>
+__device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const pp_params& P,
+                                               const PrepV& pv, const pp_result& out, const double* rec,
+                                               int64_t s, int K, int ng, uint64_t m0, uint64_t m1,
+                                               const double* pcr, const double* psr) {
+    const int64_t S = in.n_scenes;
+    const int N = P.n_points;
+    const int64_t rstride = (int64_t)(N - K) * S;
+    {   // the kept previous points: every load issued before the first store
+        double kx[PP_PREV_KEEP], ky[PP_PREV_KEEP];
+#pragma unroll
+        for (int i = 0; i < PP_PREV_KEEP; i++)
+            if (i < K) { kx[i] = in.prev_x[(int64_t)i * S + s]; ky[i] = in.prev_y[(int64_t)i * S + s]; }
+#pragma unroll
+        for (int i = 0; i < PP_PREV_KEEP; i++)
+            if (i < K) { out.next_x[(int64_t)i * S + s] = kx[i]; out.next_y[(int64_t)i * S + s] = ky[i]; }
+    }
+    double cx = pv.pos_x[s], cy = pv.pos_y[s];
+    double ca = pv.ca_p[s], sa = pv.sa_p[s];
+    double pxp = 0, pyp = 0;                       // local position before the step
+    for (int g0 = 0; g0 < ng; g0 += kChunk) {
+        double px_[kChunk], py_[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            const int g = g0 + u;
+#ifdef PP_CHECK
+            if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 19); }
+#endif
+            px_[u] = g < ng ? rec[(int64_t)g * S + s] : 0.0;
+            py_[u] = g < ng ? rec[rstride + (int64_t)g * S + s] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            const int g = g0 + u;
+            if (g >= ng) break;
+            if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
+                const double cr = pcr[g], sr = psr[g];
+                const double tpx = (pxp * ca - pyp * sa) + cx;
+                const double tpy = (pxp * sa + pyp * ca) + cy;
+                const double vx = cx - tpx, vy = cy - tpy;
+                cx = tpx + (vx * cr - vy * sr);
+                cy = tpy + (vx * sr + vy * cr);
+                const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
+                ca = nca; sa = nsa;
+            }
+            const double tx = px_[u] * ca - py_[u] * sa;
+            const double ty = px_[u] * sa + py_[u] * ca;
+            if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
+            out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
+            out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+            pxp = px_[u];
+            pyp = py_[u];
+        }
+    }
+    for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
+}
+
 // ------------------------------------------------------------------------------------------------
 // K2: candidates. One workgroup = SPB scenes x C candidates; slots in LDS.
 // kSlow = false: every scene except those flagged kLimSlow by k_prep (no library call in the
@@ -1442,7 +1504,8 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
 template <bool kSlow, int kMode>
 __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
                                            const PrepV& pv, const pp_result& out, int SPB, int BPS,
-                                           double* rec, uint64_t* adjm, int64_t g, double* sm) {
+                                           double* rec, uint64_t* adjm, int64_t g, double* sm,
+                                           int emit_in) {
     const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int C = D * Cv;                     // candidates per scene (all draws)
@@ -1468,6 +1531,9 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     // per scene: any of its draws flagged kLimSlow (absurd heading, or a speed or ramp time outside
     // the range of the unchecked divisions) -> the scene runs in the k_cand<true> instantiation
     uint32_t* sSlow = sFlags + SPB;
+    // kMode 1 with emit_in: each winner's step count and adjusted-step masks for the in-block K4
+    uint64_t* sAdj = (uint64_t*)(((uintptr_t)(sSlow + SPB) + 7) & ~(uintptr_t)7);
+    int* sNg = (int*)(sAdj + 2 * SPB);
     if (tid < SPB) { sFlags[tid] = 0; sSlow[tid] = 0; }
 #ifdef PP_CHECK
     for (int i = tid; i < 5 * nslot * kKP; i += (int)blockDim.x) sX[i] = __builtin_nan("");
@@ -1625,7 +1691,11 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
             R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
                                                        S, nullptr, 0, winner, rec + s);
-            if (winner && PP_CHK(s < g_lim.nscen, 12, s) && PP_CHKP(adjm + S + s, adjm, nadj, 13)) {
+            if (winner && emit_in) {          // in-block K4 below: step count and masks in LDS
+                out.n_out[s] = K + R.ng;
+                out.winner[s] = c;
+                sNg[sc_l] = R.ng; sAdj[2 * sc_l] = R.adj0; sAdj[2 * sc_l + 1] = R.adj1;
+            } else if (winner && PP_CHK(s < g_lim.nscen, 12, s) && PP_CHKP(adjm + S + s, adjm, nadj, 13)) {
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
                 adjm[s] = R.adj0;
@@ -1644,11 +1714,38 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         atomicOr(&sFlags[sc_l], flags);
     }
     __syncthreads();
-    if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
+    if (tid < nsc && ((sSlow[tid] != 0) == kSlow) && PP_CHK(s0 + tid < g_lim.nscen, 15, s0 + tid)) {
         const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
-        if (!PP_CHK(s0 + tid < g_lim.nscen, 15, s0 + tid)) return;
         if (BPS == 1) out.status[s0 + tid] = st;
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
+    }
+    if (kMode == 1 && emit_in) {
+        // K4 in the block (reference mode): the spline slots are free now, so the team computes
+        // the sin/cos of every recorded turn of the block's winners into them (one item per
+        // winner x step), then each winner lane replays its transform from its own record
+        // (emit_scene_pre: the chain of turns and points only, emit_scene's operations).
+        double* pcr = sm;
+        double* psr = sm + SPB * N;               // 2 SPB N <= 5 NL SPB kKP doubles (host: emit_in)
+        for (int idx = tid; idx < nsc * N; idx += (int)blockDim.x) {
+            const int w = idx / N, gs = idx - w * N;
+            if (((sSlow[w] != 0) != kSlow) || gs >= sNg[w]) continue;
+            const uint64_t mm = gs < 64 ? sAdj[2 * w] : sAdj[2 * w + 1];
+            if (!((mm >> (gs & 63)) & 1)) continue;
+            const int64_t s = s0 + w;
+            const double* rr = rec + 2 * (int64_t)(N - pv.K[s]) * S + (int64_t)gs * S + s;
+            if (!PP_CHKP(rr, rec, nrec, 18)) continue;
+            const double rt = *rr;
+            double sr, cr;
+            if (fabs(rt) <= ppm::kMediumMax) ppm::sincos_pp<false>(rt, sr, cr);
+            else ppm::sincos_pp<true>(rt, sr, cr);
+            pcr[idx] = cr; psr[idx] = sr;
+        }
+        __syncthreads();
+        if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
+            const int64_t s = s0 + tid;
+            emit_scene_pre<PP_EMIT_CHUNK>(in, P, pv, out, rec, s, pv.K[s], sNg[tid], sAdj[2 * tid],
+                                          sAdj[2 * tid + 1], pcr + tid * N, psr + tid * N);
+        }
     }
 }
 
@@ -1660,17 +1757,17 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
-                                              uint32_t* gbits, int64_t ngroups) {
+                                              uint32_t* gbits, int64_t ngroups, int emit_in) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (!kSlow) {
-        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm);
+        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm, emit_in);
         return;
     }
     for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
         const uint32_t word = gbits[g >> 5];                      // same address for every lane
         if (!((word >> (g & 31)) & 1u)) continue;
         __syncthreads();                                          // the previous group's LDS readers are done
-        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
+        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm, emit_in);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
@@ -1897,14 +1994,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         uint64_t* adjm, uint32_t* gbits) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int64_t g = blockIdx.x;
-    cand_group<false, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+    cand_group<false, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm, 1);
     __syncthreads();
     if ((gbits[g >> 5] >> (g & 31)) & 1u) {                   // same word for every lane
-        cand_group<true, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+        cand_group<true, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm, 1);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
-    const int64_t s = g * SPB + threadIdx.x;
-    if ((int)threadIdx.x < SPB && s < in.n_scenes) emit_scene<16>(in, P, pv, out, rec, adjm, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2287,6 +2382,13 @@ PrepV prep_bind(void* base, int64_t S) {
 // K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
 // SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. pp_set_prep_group (or
 // the PP_PREP_G environment variable) forces a value.
+// K4 inside k_cand: the winners' sin/cos tables (2 N doubles each) fit the block's spline slots;
+// PP_EMIT_IN=0 forces the k_emit kernel (A/B, tests)
+bool emit_in_ok(int N) {
+    const char* e = getenv("PP_EMIT_IN");
+    if (e && *e && atoi(e) == 0) return false;
+    return 2 * N <= 5 * NL * kKP;
+}
 // k_cand_small (K2 + K4 in one launch) up to this many scenes; PP_FUSED=0/1 forces it off/on (A/B)
 constexpr int64_t kFusedSmall = 16384;
 bool fused_small(int64_t S) {
@@ -2364,7 +2466,9 @@ CandGeom cand_geom(int C, int64_t S) {
     g.bps = C <= 256 ? 1 : (C + 255) / 256;
     g.threads = C <= 256 ? ((g.spb * C + 63) / 64) * 64 : 256;
     const int nslot = NL * g.spb;
+    // slots (5 x kKP doubles + 4 ints each), sFlags/sSlow, then (8-aligned) sAdj and sNg
     g.lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * g.spb;
+    g.lds = ((g.lds + 7) & ~(size_t)7) + sizeof(uint64_t) * 2 * g.spb + sizeof(int) * g.spb;
     g.groups = g.bps == 1 ? (S + g.spb - 1) / g.spb : S * g.bps;
     return g;
 }
@@ -2583,8 +2687,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const bool ref_direct = prm->cost_mode == PP_COST_REFERENCE && Dn == 1;
     const CandGeom cg = cand_geom(Dn * NL * prm->n_speeds, S);
     if (cg.groups > 0x7fffffff) return PP_ERR_ARG;
-    // small batches in reference mode: K2 and K4 in one launch (k_cand_small)
-    const bool fused = ref_direct && !prm->emit_paths && cg.bps == 1 && fused_small(S);
+    // small batches in reference mode without paths: K2 and K4 in one launch (k_cand_small, K4 in
+    // the block: emit_in), unless the horizon's sin/cos table (2 N doubles per winner) exceeds the
+    // block's spline slots. Large batches keep K4 in its own kernel: in the block, the serial
+    // replay holds the block's LDS and costs k_cand more than k_emit takes.
+    const bool fused = ref_direct && !prm->emit_paths && cg.bps == 1 && emit_in_ok(prm->n_points) &&
+                       fused_small(S);
+    const bool emit_in = fused;
     // the map lock is held from workspace binding through the (asynchronous) launches: a
     // concurrent call cannot grow and free this stream's buffers in between
     std::lock_guard<std::mutex> lk(M->mu);
@@ -2622,7 +2731,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             DS.ev_pool.pop_back();
             DS.ev_rec.push_back(ev[i]);
         }
-        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) && !fused ? 1 : 0);
+        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0);
     }
     pp_params P = *prm;
     pp_scene_batch B = *in;
@@ -2675,9 +2784,10 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (timing) (void)hipEventRecord(ev[1], st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng);                                         \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, ei);                                     \
         hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng)
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, ei)
+        const int ei = emit_in ? 1 : 0;
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
         else if (ref_direct && fused) {
             hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
@@ -2689,7 +2799,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
-    if (ref_direct && !P.emit_paths && !fused) {
+    if (ref_direct && !P.emit_paths && !emit_in) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
             const int64_t blocks = (S + 63) / 64;
             hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm);

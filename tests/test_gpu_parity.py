@@ -311,10 +311,12 @@ def test_prep_group_invariance(env, case):
 
 @pytest.mark.parametrize("case", ["random", "speed_edges"])
 def test_fused_small_invariance(env, case, monkeypatch):
-    """Small reference-mode batches run K2 and K4 in one launch (k_cand_small: the group's fast
-    scenes, its flagged scenes, then the winner lanes' output transform); PP_FUSED=0 forces the
-    three-launch path (k_cand<false>, k_cand<true>, k_emit). Both give bit-identical outputs and
-    equal the oracle. speed_edges: scenes flagged for the checked instantiation in most groups."""
+    """Reference mode without paths writes next_x/next_y in two ways: small batches run K2 and K4
+    in one launch (k_cand_small: the group's fast scenes, its flagged scenes, then the block's team
+    computes the recorded turns' sin/cos into the freed spline slots and each winner lane replays
+    its record), large ones (and PP_FUSED=0) run k_cand<false>, k_cand<true> and k_emit. Both give
+    bit-identical outputs and equal the oracle. speed_edges: scenes flagged for the checked
+    instantiation in most groups."""
     S = 1200
     sc = ppamd.synth_host(env["m"], S, seed=515, first=99)
     if case == "speed_edges":
@@ -325,10 +327,10 @@ def test_fused_small_invariance(env, case, monkeypatch):
     d = to_dev(env, sc)
     prm = ppamd.default_params()
     outs = {}
-    for f in ("0", "1"):
+    for name, f in (("k_emit", "0"), ("fused", "1")):
         monkeypatch.setenv("PP_FUSED", f)
-        outs[f] = run_gpu(env, d, prm)
-    for k, v in outs["0"].items():
-        assert np.array_equal(outs["1"][k], v, equal_nan=v.dtype.kind == "f"), k
+        outs[name] = run_gpu(env, d, prm)
+    for k, v in outs["k_emit"].items():
+        assert np.array_equal(outs["fused"][k], v, equal_nan=v.dtype.kind == "f"), k
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
-    compare(outs["1"], ref)
+    compare(outs["fused"], ref)
