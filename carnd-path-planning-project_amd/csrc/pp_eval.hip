@@ -111,6 +111,18 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_SPL_A0              // cached spline segment: extrapolation folded into the cubic form
 #define PP_SPL_A0 1
 #endif
+// PP_NT: the winner record (written once by k_cand, read once by k_emit) and next_x/next_y
+// (written once) as nontemporal (streaming) accesses
+#ifndef PP_NT
+#define PP_NT 1
+#endif
+#if PP_NT
+#define PP_ST(p, v) __builtin_nontemporal_store((v), (p))
+#define PP_LD(p) __builtin_nontemporal_load(p)
+#else
+#define PP_ST(p, v) (*(p) = (v))
+#define PP_LD(p) (*(p))
+#endif
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
@@ -1115,7 +1127,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
                 if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
             }
-            if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
+            if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
             ng++;
             R.travelled += dstep;
         }
@@ -1336,7 +1348,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                                         : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
                     if (PP_CHKP(rec + 2 * rstride + ng * ws, rec, nrec, 6))
-                        rec[2 * rstride + ng * ws] = nad - adiff;   // rot (src/main.cpp:986)
+                        PP_ST(rec + 2 * rstride + ng * ws, nad - adiff);   // rot (src/main.cpp:986)
                     const uint64_t bit = 1ull << (ng & 63);
                     if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
                 }
@@ -1380,7 +1392,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 *(double2*)(px + ng * ps) = make_double2(tx + cx, ty + cy);     // one 16-B store (x, y)
         }
-        if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { rec[ng * ws] = pos_x; rec[rstride + ng * ws] = pos_y; }
+        if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -1446,7 +1458,7 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
             if (i < K) { kx[i] = in.prev_x[(int64_t)i * S + s]; ky[i] = in.prev_y[(int64_t)i * S + s]; }
 #pragma unroll
         for (int i = 0; i < PP_PREV_KEEP; i++)
-            if (i < K) { out.next_x[(int64_t)i * S + s] = kx[i]; out.next_y[(int64_t)i * S + s] = ky[i]; }
+            if (i < K) { PP_ST(out.next_x + (int64_t)i * S + s, kx[i]); PP_ST(out.next_y + (int64_t)i * S + s, ky[i]); }
     }
     double cx = pv.pos_x[s], cy = pv.pos_y[s];
     double ca = pv.ca_p[s], sa = pv.sa_p[s];
@@ -1459,8 +1471,8 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 #ifdef PP_CHECK
             if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 19); }
 #endif
-            px_[u] = g < ng ? rec[(int64_t)g * S + s] : 0.0;
-            py_[u] = g < ng ? rec[rstride + (int64_t)g * S + s] : 0.0;
+            px_[u] = g < ng ? PP_LD(rec + (int64_t)g * S + s) : 0.0;
+            py_[u] = g < ng ? PP_LD(rec + rstride + (int64_t)g * S + s) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
@@ -1479,8 +1491,8 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
             const double tx = px_[u] * ca - py_[u] * sa;
             const double ty = px_[u] * sa + py_[u] * ca;
             if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
-            out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
-            out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+            PP_ST(out.next_x + (int64_t)(K + g) * S + s, tx + cx);
+            PP_ST(out.next_y + (int64_t)(K + g) * S + s, ty + cy);
             pxp = px_[u];
             pyp = py_[u];
         }
@@ -1857,7 +1869,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             if (i < K) { kx[i] = in.prev_x[(int64_t)i * S + s]; ky[i] = in.prev_y[(int64_t)i * S + s]; }
 #pragma unroll
         for (int i = 0; i < PP_PREV_KEEP; i++)
-            if (i < K) { out.next_x[(int64_t)i * S + s] = kx[i]; out.next_y[(int64_t)i * S + s] = ky[i]; }
+            if (i < K) { PP_ST(out.next_x + (int64_t)i * S + s, kx[i]); PP_ST(out.next_y + (int64_t)i * S + s, ky[i]); }
     }
     double cx = pv.pos_x[s], cy = pv.pos_y[s], tangle = pv.angle[s];
     double ca = pv.ca_p[s], sa = pv.sa_p[s];
@@ -1897,9 +1909,9 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 16); }
             if (bit) { PP_CHKP(rec + 2 * rstride + (int64_t)g * S + s, rec, nrec, 16); }
 #endif
-            px_[u] = g < ng ? rec[(int64_t)g * S + s] : 0.0;
-            py_[u] = g < ng ? rec[rstride + (int64_t)g * S + s] : 0.0;
-            rt[u] = bit ? rec[2 * rstride + (int64_t)g * S + s] : 0.0;
+            px_[u] = g < ng ? PP_LD(rec + (int64_t)g * S + s) : 0.0;
+            py_[u] = g < ng ? PP_LD(rec + rstride + (int64_t)g * S + s) : 0.0;
+            rt[u] = bit ? PP_LD(rec + 2 * rstride + (int64_t)g * S + s) : 0.0;
         }
         bool huge = false;
 #pragma unroll
@@ -1935,8 +1947,8 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             const double tx = px_[u] * ca - py_[u] * sa;
             const double ty = px_[u] * sa + py_[u] * ca;
             if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
-            out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
-            out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
+            PP_ST(out.next_x + (int64_t)(K + g) * S + s, tx + cx);
+            PP_ST(out.next_y + (int64_t)(K + g) * S + s, ty + cy);
             pxp = px_[u];
             pyp = py_[u];
         }
