@@ -658,6 +658,111 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAV
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
 }
 
+// K1 with the cars staged in LDS (large batches, no car table, <= kStRows rows, map in LDS): every
+// car field is read once, coalesced, in row order. Pass 1 visits the cars nearest first (the
+// divergence argument of k_prep) but reads their x, y from LDS, and leaves each car's Frenet
+// (s, d) in place of its x, y with (matched, lane, next waypoint) beside it; pass 2 reads id, vx,
+// vy in row order (the reference's own iteration order, src/main.cpp:1325-1411), projects the
+// velocity and feeds the planner. 512-lane blocks, 2 waves per SIMD: one map copy per CU beside
+// 12 x 512 staged (x, y) pairs (PP_PREP_ST).
+constexpr int kStRows = 12;
+constexpr int kStBlock = 512;
+template <int kUnused>
+__global__ __launch_bounds__(kStBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_prep_st(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_scene_info* info, uint32_t* out_status,
+        GroupBits gb) {
+    extern __shared__ __attribute__((aligned(16))) double smap[];
+    const int n = mg.n;
+    for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
+    double2* sxy = (double2*)(smap + ((kMapArrays * n + 1) & ~1));       // [row][lane]
+    int32_t* smeta = (int32_t*)(sxy + kStRows * kStBlock);                // [row][lane]
+    __syncthreads();
+    const MapV m = map_view(smap, n, mg.fastm);
+    const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= Sv) return;
+    const int64_t s = D == 1 ? v : v / D;
+    const int draw = (int)(v - s * D);
+    const int tid = threadIdx.x;
+
+    EgoSt e;
+    prep_ego<1>(m, in, P, S, s, 0, e);
+    uint32_t status = e.status;
+    const int T_in = in.prev_target_lane[s];
+    int ncar = in.n_cars[s];
+    if (ncar > in.car_stride) ncar = in.car_stride;
+    // stage x, y (row order, coalesced) and the nearest-first keys (k_prep's)
+    uint32_t key[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        key[j] = 0xFFFFFFF0u | (uint32_t)j;
+        if (j < kStRows && j < ncar) {
+            const int64_t ix = (int64_t)j * S + s;
+            double cx = in.car_x[ix], cy = in.car_y[ix];
+            if (draw > 0) {
+                const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+                cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 0);
+                cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 1);
+            }
+            sxy[j * kStBlock + tid] = make_double2(cx, cy);
+            const double dx = cx - e.ego_x, dy = cy - e.ego_y;
+            const float f = (float)(dx * dx + dy * dy);
+            key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
+        }
+    }
+#pragma unroll
+    for (int pw = 1; pw < 16; pw <<= 1)
+#pragma unroll
+        for (int k = pw; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % pw; j < 16 - k; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; i++)
+                    if ((i + j) / (2 * pw) == (i + j + k) / (2 * pw)) {
+                        const uint32_t lo = key[i + j] < key[i + j + k] ? key[i + j] : key[i + j + k];
+                        const uint32_t hi = key[i + j] < key[i + j + k] ? key[i + j + k] : key[i + j];
+                        key[i + j] = lo; key[i + j + k] = hi;
+                    }
+    uint64_t order = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
+    // pass 1: Frenet matching, nearest first, from LDS
+    for (int kk = 0; kk < ncar; kk++) {
+        const int it = (int)((order >> (4 * kk)) & 15);
+        const double2 xy = sxy[it * kStBlock + tid];
+        double cs, cd;
+        int clane = 0, nwp = 0;
+        int32_t meta = 0;        // matched | lane << 1 | next waypoint * 16 (may be negative)
+        if (lane_match(m, e.ref_wp, e.ratio, xy.x, xy.y, cs, cd, clane, nwp)) {
+            sxy[it * kStBlock + tid] = make_double2(cs, cd);
+            meta = 1 | (clane << 1) | (int32_t)((uint32_t)nwp << 4);
+        }
+        smeta[it * kStBlock + tid] = meta;
+    }
+    // pass 2: row order (the reference's), velocity projection and the planner
+    PlanAcc a;
+    a.init();
+    for (int j = 0; j < ncar; j++) {
+        const int64_t ix = (int64_t)j * S + s;
+        const int id = in.car_id[ix];
+        double cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+        const int32_t meta = smeta[j * kStBlock + tid];
+        if (!(meta & 1)) { status |= PP_ST_CAR_UNMATCHED; continue; }
+        if (draw > 0) {
+            const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
+            cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 2);
+            cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 3);
+        }
+        const double2 sd = sxy[j * kStBlock + tid];
+        double cvs, cvd;
+        project_speed(m, cvx, cvy, meta >> 4, cvs, cvd);       // arithmetic shift: nwp
+        a.add(P, e, T_in, j, id, sd.x, sd.y, (meta >> 1) & 7, cvs, cvd);
+    }
+    prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, false, 0, T_in, e, a, status);
+}
+
 // K1 for small batches: a group of G lanes per evaluation (G = 2 ... 16; kernels k_prep_g2 ... k_prep_g16), so that a batch of a few
 // thousand scenes still fills the chip (BASELINE config 2: 4,096 scenes). Lane r of a group matches
 // rows r, r + G, ... (coalesced across the group) and scans every G-th waypoint for the Frenet
@@ -2407,6 +2512,18 @@ bool fused_small(int64_t S) {
     const char* e = getenv("PP_FUSED");
     return e && *e ? atoi(e) != 0 : S <= kFusedSmall;
 }
+// k_prep_st (cars staged in LDS): its LDS (map, then 16-B aligned (x, y) pairs and the match words).
+// Off by default: it reads the scene record once (FETCH 0.57 GB raw per 2M-scene launch against
+// the gathering k_prep's 4.0 GB, whose re-reads the Infinity Cache serves) but its LDS allows 2 waves
+// per SIMD instead of 3, and it takes 2.75 ms against 2.05. PP_PREP_ST=1 selects it.
+constexpr size_t kLdsMaxBlock = 163840;
+size_t prep_st_lds(int n) {
+    return sizeof(double) * (size_t)((kMapArrays * n + 1) & ~1) + (16 + 4) * (size_t)kStRows * kStBlock;
+}
+bool prep_st_on() {
+    const char* e = getenv("PP_PREP_ST");
+    return e && *e ? atoi(e) != 0 : false;
+}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
@@ -2779,7 +2896,17 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
 #define PP_LAUNCH_PREP(KER) \
         if (lmap) hipLaunchKernelGGL(KER<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb); \
         else hipLaunchKernelGGL(KER<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb)
-        switch (G) {
+        const size_t lds_st = prep_st_lds(mg.n);
+        if (G == 1 && !B.tab_valid && lmap && B.car_stride <= kStRows && lds_st <= kLdsMaxBlock &&
+            prep_st_on()) {
+            static std::once_flag attr_once;     // dynamic LDS beyond 64 KB (one workgroup may hold 160 KB)
+            std::call_once(attr_once, [] {
+                (void)hipFuncSetAttribute((const void*)k_prep_st<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)kLdsMaxBlock);
+            });
+            hipLaunchKernelGGL(k_prep_st<0>, dim3((unsigned)((Sv + kStBlock - 1) / kStBlock)), dim3(kStBlock),
+                               lds_st, st, mg, B, P, pv, R.info, R.status, gb);
+        } else switch (G) {
             case 2: { PP_LAUNCH_PREP(k_prep_g2); break; }
             case 4: { PP_LAUNCH_PREP(k_prep_g4); break; }
             case 8: { PP_LAUNCH_PREP(k_prep_g8); break; }

@@ -334,3 +334,43 @@ def test_fused_small_invariance(env, case, monkeypatch):
         assert np.array_equal(outs["fused"][k], v, equal_nan=v.dtype.kind == "f"), k
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
     compare(outs["fused"], ref)
+
+
+@pytest.mark.parametrize("case", ["random", "ties_ids", "draws"])
+def test_prep_staged_invariance(env, case, monkeypatch):
+    """K1 on large batches stages every car's x, y in LDS (k_prep_st: coalesced row-order loads,
+    matching nearest first from LDS, planner pass in row order); PP_PREP_ST=0 forces the gathering
+    k_prep. Both give bit-identical outputs (scene info included) and equal the oracle. Cases:
+    random scenes; tied duplicate cars with -1, negative and large ids; Monte-Carlo draws (the
+    position noise applied where x, y are staged, the velocity noise in the row-order pass)."""
+    S = 1500
+    sc = ppamd.synth_host(env["m"], S, seed=4711, first=123)
+    kw = {"emit_paths": True}
+    if case == "ties_ids":
+        for j in range(6, 12):
+            for k in ("car_x", "car_y", "car_vx", "car_vy"):
+                sc[k][j, ::2] = sc[k][j - 6, ::2]
+        sc["car_id"][:, 1::4] = (np.arange(12) * 1000 + 1000)[:, None]
+        sc["car_id"][0, 3::4] = -1
+    if case == "draws":
+        kw = {"n_speeds": 1, "n_draws": 8, "noise_seed": 5}
+    prm = ppamd.default_params(**kw)
+    d = to_dev(env, sc)
+    outs = {}
+    try:
+        ppamd.set_prep_group(1)          # one lane per evaluation at this size too
+        for f in ("0", "1"):
+            monkeypatch.setenv("PP_PREP_ST", f)
+            outs[f] = run_gpu(env, d, prm, info=case != "draws")
+    finally:
+        ppamd.set_prep_group(0)
+
+    def same(a, b):
+        if a.dtype.names:
+            return all(same(a[f], b[f]) for f in a.dtype.names)
+        return np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+    for k, v in outs["0"].items():
+        assert same(outs["1"][k], v), k
+    if case != "draws":
+        ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+        compare(outs["1"], ref)

@@ -1,19 +1,29 @@
 #!/bin/bash
-# Full round measurement on the GPU box (repo root): GPU parity tests, PMC passes summarised into
-# profiles/pmc_summary.json, then the default bench line (reads that summary for roofline.traffic)
-# and the rocprofv3 kernel-trace stats of the same command. Outputs under gpurun_out/<tag>/.
-set -e
-TAG=${1:-r01}
+# Full round measurement on the GPU box (repo root): GPU parity tests and smoke, PMC passes
+# summarised into profiles/pmc_summary.json (config 5 and config 3), the default bench line (reads
+# that summary for roofline.traffic / traffic_pipeline), the rocprofv3 kernel-trace stats of the
+# same command, and the other BASELINE configurations. Outputs under gpurun_out/<tag>/.
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -eo pipefail
+TAG=${1:-r02}
 OUT=gpurun_out/$TAG
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-tail -2 $OUT/gpu_tests.log
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
 bash tools/pmc.sh $OUT/pmc
 python3 tools/pmc_summarize.py $OUT/pmc k_cand_S2097152_C15_N50 > $OUT/pmc_summary.txt
+bash tools/pmc.sh $OUT/pmc3 --steps 2 --warmup 1 --no-cpu-baseline --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
+python3 tools/pmc_summarize.py $OUT/pmc3 k_cand_S262144_C24_N100_paths > $OUT/pmc3_summary.txt
 cp profiles/pmc_summary.json $OUT/pmc_summary.json
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
-tail -1 $OUT/bench.json | cut -c1-400
+tail -1 $OUT/bench.json | cut -c1-300
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/stats -o run -- python3 $ROOT/bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.err
 echo "rocprof done"
+run() { name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err; echo "$name: $(tail -1 $OUT/$name.json | cut -c1-200)"; }
+run bench_config2 --scenes 4096 --steps 300 --warmup 30 --no-cpu-baseline
+run bench_config3_allpaths --emit-paths --n-speeds 8 --n-points 100 --scenes 262144 --no-cpu-baseline
+run bench_config4_montecarlo --draws 64 --n-speeds 1 --scenes 16384 --no-cpu-baseline
