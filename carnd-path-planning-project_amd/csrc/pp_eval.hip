@@ -1618,11 +1618,11 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 // One group g of the candidate grid (BPS == 1: scenes [g SPB, g SPB + SPB); BPS > 1: candidates
 // [coff, coff + 256) of scene g / BPS) by the whole workgroup. Every barrier inside is reached by
 // all threads of the block (the early return is block-uniform).
-template <bool kSlow, int kMode>
+template <bool kSlow, int kMode, bool kEmitIn = false>
 __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
                                            const PrepV& pv, const pp_result& out, int SPB, int BPS,
-                                           double* rec, uint64_t* adjm, int64_t g, double* sm,
-                                           int emit_in) {
+                                           double* rec, uint64_t* adjm, int64_t g, double* sm) {
+    constexpr bool emit_in = kEmitIn && kMode == 1;
     const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int C = D * Cv;                     // candidates per scene (all draws)
@@ -1874,17 +1874,17 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
-                                              uint32_t* gbits, int64_t ngroups, int emit_in) {
+                                              uint32_t* gbits, int64_t ngroups) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (!kSlow) {
-        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm, emit_in);
+        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm);
         return;
     }
     for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
         const uint32_t word = gbits[g >> 5];                      // same address for every lane
         if (!((word >> (g & 31)) & 1u)) continue;
         __syncthreads();                                          // the previous group's LDS readers are done
-        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm, emit_in);
+        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
@@ -2111,10 +2111,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         uint64_t* adjm, uint32_t* gbits) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int64_t g = blockIdx.x;
-    cand_group<false, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm, 1);
+    cand_group<false, 1, true>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
     __syncthreads();
     if ((gbits[g >> 5] >> (g & 31)) & 1u) {                   // same word for every lane
-        cand_group<true, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm, 1);
+        cand_group<true, 1, true>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
@@ -2923,10 +2923,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (timing) (void)hipEventRecord(ev[1], st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, ei);                                     \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng);                                         \
         hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, ei)
-        const int ei = emit_in ? 1 : 0;
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng)
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
         else if (ref_direct && fused) {
             hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
