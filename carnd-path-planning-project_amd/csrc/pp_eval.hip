@@ -462,7 +462,7 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
     if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
     if (!ok) lim_mask |= kLimSlow;
-    if ((lim_mask & kLimSlow) && r == 0) {
+    if ((lim_mask & kLimSlow) && r == 0 && gb.bits) {   // (k_step_small: no bitmap)
         const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
         for (int b = 0; b < gb.BPS; b++) atomicOr(&gb.bits[(g0 + b) >> 5], 1u << ((g0 + b) & 31));
     }
@@ -769,6 +769,10 @@ __global__ __launch_bounds__(kStBlock) __attribute__((amdgpu_waves_per_eu(2, 2))
 // frame; the planner's pass then runs over each round's G cars in ascending row order on every
 // lane of the group (the cars' Frenet states exchanged by lane shuffles), i.e. in the reference's
 // own iteration order. No car table (pp_eval picks k_prep for table mode).
+template <int G>
+__device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                              const PrepV& pv, pp_scene_info* info, uint32_t* out_status,
+                                              const GroupBits& gb, int64_t v, int r);
 template <bool kLdsMap, int G>
 __device__ __forceinline__ void prep_grp_body(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
@@ -780,12 +784,21 @@ __device__ __forceinline__ void prep_grp_body(MapG mg, pp_scene_batch in, pp_par
         __syncthreads();
     }
     const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
-    const int64_t S = in.n_scenes;
-    const int D = P.n_draws > 1 ? P.n_draws : 1;
-    const int64_t Sv = S * D;
+    const int64_t Sv = in.n_scenes * (P.n_draws > 1 ? P.n_draws : 1);
     const int r = (int)(threadIdx.x % G);
     const int64_t v = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
     if (v >= Sv) return;                      // whole groups leave together
+    prep_grp_eval<G>(m, in, P, pv, info, out_status, gb, v, r);
+}
+
+// One evaluation v by the G lanes of a group (this one is lane r); every lane of the group runs it
+template <int G>
+__device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                              const PrepV& pv, pp_scene_info* info, uint32_t* out_status,
+                                              const GroupBits& gb, int64_t v, int r) {
+    const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
     const int64_t s = D == 1 ? v : v / D;
     const int draw = (int)(v - s * D);
 
@@ -2120,6 +2133,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 }
 
 // ------------------------------------------------------------------------------------------------
+// The whole step in one launch for small batches in reference mode (BASELINE config 2): K1 for the
+// block's SPB (<= 16) scenes with 16 lanes each (prep_grp_eval<16>, the map staged in LDS once),
+// a barrier, then k_cand_small's body (fast scenes, flagged scenes, the winners' replay), its
+// phase A reading the same LDS map. The prep record goes through global memory inside the block
+// (written, barrier, read by the same workgroup). No kernel boundary is left in the step.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int n = mg.n;
+    for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) sm[i] = mg.buf[i];
+    __syncthreads();
+    const MapV m = map_view(sm, n, mg.fastm);
+    const int64_t g = blockIdx.x;
+    {   // K1: scene g SPB + threadIdx.x / 16 by a group of 16 lanes
+        const int q = (int)threadIdx.x / 16;
+        const int64_t v = g * SPB + q;
+        const GroupBits nobits = {nullptr, SPB, 1};
+        if (q < SPB && v < in.n_scenes) prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, v, (int)threadIdx.x % 16);
+    }
+    __syncthreads();
+    const MapG ml = {sm, n, mg.fastm};
+    double* csm = sm + ((kMapArrays * n + 1) & ~1);
+    cand_group<false, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
+    __syncthreads();
+    cand_group<true, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
+}
+
+// ------------------------------------------------------------------------------------------------
 // closed-loop rollout: the simulator shim (include/pp.h pp_rollout). One lane per scene: log the
 // frame, drive `consume` points of the plan, advance the traffic, report the cars in range.
 // ------------------------------------------------------------------------------------------------
@@ -2524,6 +2567,12 @@ bool prep_st_on() {
     const char* e = getenv("PP_PREP_ST");
     return e && *e ? atoi(e) != 0 : false;
 }
+// k_step_small (K1 + K2 + K4 in one launch for the batches k_cand_small takes); PP_STEP_FUSED=0
+// falls back to k_prep_g* + k_cand_small (A/B, tests)
+bool step_fused_on() {
+    const char* e = getenv("PP_STEP_FUSED");
+    return e && *e ? atoi(e) != 0 : true;
+}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
@@ -2589,15 +2638,19 @@ void free_ws(StreamWS& W) {
 // k_cand's launch geometry for C candidates per scene (BPS == 1: SPB scenes per group; else one
 // scene over BPS groups of 256 candidates)
 struct CandGeom { int spb, bps, threads; size_t lds; int64_t groups; };
+// k_cand's LDS for SPB scenes per group: slots (5 x kKP doubles + 4 ints each), sFlags/sSlow,
+// then (8-aligned) sAdj and sNg
+size_t cand_geom_lds(int spb) {
+    const int nslot = NL * spb;
+    size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * spb;
+    return ((lds + 7) & ~(size_t)7) + sizeof(uint64_t) * 2 * spb + sizeof(int) * spb;
+}
 CandGeom cand_geom(int C, int64_t S) {
     CandGeom g;
     g.spb = C <= 256 ? cands_per_block(C) : 1;
     g.bps = C <= 256 ? 1 : (C + 255) / 256;
     g.threads = C <= 256 ? ((g.spb * C + 63) / 64) * 64 : 256;
-    const int nslot = NL * g.spb;
-    // slots (5 x kKP doubles + 4 ints each), sFlags/sSlow, then (8-aligned) sAdj and sNg
-    g.lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * g.spb;
-    g.lds = ((g.lds + 7) & ~(size_t)7) + sizeof(uint64_t) * 2 * g.spb + sizeof(int) * g.spb;
+    g.lds = cand_geom_lds(g.spb);
     g.groups = g.bps == 1 ? (S + g.spb - 1) / g.spb : S * g.bps;
     return g;
 }
@@ -2881,6 +2934,20 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             hipMemcpyToSymbol(HIP_SYMBOL(g_lim), &L, sizeof L) != hipSuccess) return PP_ERR_HIP;
     }
 #endif
+    // small reference-mode batches with the map in LDS: the whole step in one launch (k_step_small)
+    const int spb_f = std::min(cg.spb, 256 / 16);
+    const int64_t groups_f = (S + spb_f - 1) / spb_f;
+    const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * mg.n + 1) & ~1);
+    const size_t lds_f = map_lds + cand_geom_lds(spb_f);
+    const bool step_fused = fused && !B.tab_valid && mg.n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
+    if (step_fused) {
+        if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
+        hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(cg.threads), lds_f, st, mg, B, P, pv,
+                           R, spb_f, rec, adjm);
+        if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
+        if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+        return PP_OK;
+    }
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
         const int threads = 256;

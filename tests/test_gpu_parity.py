@@ -311,12 +311,13 @@ def test_prep_group_invariance(env, case):
 
 @pytest.mark.parametrize("case", ["random", "speed_edges"])
 def test_fused_small_invariance(env, case, monkeypatch):
-    """Reference mode without paths writes next_x/next_y in two ways: small batches run K2 and K4
-    in one launch (k_cand_small: the group's fast scenes, its flagged scenes, then the block's team
-    computes the recorded turns' sin/cos into the freed spline slots and each winner lane replays
-    its record), large ones (and PP_FUSED=0) run k_cand<false>, k_cand<true> and k_emit. Both give
-    bit-identical outputs and equal the oracle. speed_edges: scenes flagged for the checked
-    instantiation in most groups."""
+    """Reference mode without paths has three launch shapes: small batches run the whole step in
+    one launch (k_step_small: K1 with 16 lanes per scene, then K2 and K4 in the same block), or
+    with PP_STEP_FUSED=0 K1 then K2 + K4 in one launch (k_cand_small: the group's fast scenes, its
+    flagged scenes, then the block's team computes the recorded turns' sin/cos into the freed
+    spline slots and each winner lane replays its record); large batches (and PP_FUSED=0) run
+    k_prep, k_cand<false>, k_cand<true> and k_emit. All give bit-identical outputs and equal the
+    oracle. speed_edges: scenes flagged for the checked instantiation in most groups."""
     S = 1200
     sc = ppamd.synth_host(env["m"], S, seed=515, first=99)
     if case == "speed_edges":
@@ -327,11 +328,18 @@ def test_fused_small_invariance(env, case, monkeypatch):
     d = to_dev(env, sc)
     prm = ppamd.default_params()
     outs = {}
-    for name, f in (("k_emit", "0"), ("fused", "1")):
+    for name, f, st in (("k_emit", "0", "0"), ("k_cand_small", "1", "0"), ("step", "1", "1")):
         monkeypatch.setenv("PP_FUSED", f)
-        outs[name] = run_gpu(env, d, prm)
-    for k, v in outs["k_emit"].items():
-        assert np.array_equal(outs["fused"][k], v, equal_nan=v.dtype.kind == "f"), k
+        monkeypatch.setenv("PP_STEP_FUSED", st)
+        outs[name] = run_gpu(env, d, prm, info=True)
+    def same(a, b):
+        if a.dtype.names:
+            return all(same(a[f], b[f]) for f in a.dtype.names)
+        return np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+    for name in ("k_cand_small", "step"):
+        for k, v in outs["k_emit"].items():
+            assert same(outs[name][k], v), (name, k)
+    outs["fused"] = outs["step"]
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
     compare(outs["fused"], ref)
 
