@@ -232,6 +232,9 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
     return an == 0.0 ? q0 : q;
 }
 
+#ifndef PP_MATCH_BF
+#define PP_MATCH_BF 0
+#endif
 // lane_matching on a map with fastm: the same walk, with each lane segment's rdenom and its
 // reciprocal from the tables (the division snom^2 / rdenom by div_by_rcp: the same correctly
 // rounded value), and the waypoint indices stepped instead of re-wrapped.
@@ -263,9 +266,23 @@ __device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double
             const double rn = pdx * dx + pdy * dy;
             const double snom = pdx * dy - pdy * dx;
             double rnom, dsq;
+#if PP_MATCH_BF
+            // the three cases as selects (same operations; the wave runs every case anyway when
+            // its lanes' points fall on different sides of the segment)
+            {
+                const bool lo = rn < -1, hi = !lo && rn > den;
+                const double dlo = pdx * pdx + pdy * pdy;
+                const double hx = x - bx, hy = y - by;
+                const double dhi = hx * hx + hy * hy;
+                const double din = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]);
+                rnom = lo ? 0.0 : (hi ? den : rn);
+                dsq = lo ? dlo : (hi ? dhi : din);
+            }
+#else
             if (rn < -1) { rnom = 0; dsq = pdx * pdx + pdy * pdy; }                            // :227-231
             else if (rn > den) { rnom = den; dsq = (x - bx) * (x - bx) + (y - by) * (y - by); }   // :232-236
             else { rnom = rn; dsq = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]); }
+#endif
             if (dsq < best) {
                 best = dsq;
                 improved = true;

@@ -518,8 +518,10 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
     cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
 }
 
-template <bool kLdsMap>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+// kW4: the 4-waves-per-SIMD instantiation (<= 128 VGPRs): for batches whose wave count fills
+// whole rounds of 4 waves per SIMD better than of 3 (prep_w4 in pp_eval)
+template <bool kLdsMap, bool kW4 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
@@ -1628,6 +1630,9 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 #ifndef PP_CAND_WAVES
 #define PP_CAND_WAVES 4
 #endif
+#ifndef PP_CAND_WAVES_PATHS      // emit_paths instantiations (the output transform's registers)
+#define PP_CAND_WAVES_PATHS 4
+#endif
 // One group g of the candidate grid (BPS == 1: scenes [g SPB, g SPB + SPB); BPS > 1: candidates
 // [coff, coff + 256) of scene g / BPS) by the whole workgroup. Every barrier inside is reached by
 // all threads of the block (the early return is block-uniform).
@@ -1885,7 +1890,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 // are block-uniform; a barrier separates consecutive groups' use of the block's LDS). Each group
 // clears its bit after use, so the bitmap is all zero again for the next pp_eval.
 template <bool kSlow, int kMode>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES_PATHS : PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
                                               uint32_t* gbits, int64_t ngroups) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -2573,6 +2578,24 @@ bool step_fused_on() {
     const char* e = getenv("PP_STEP_FUSED");
     return e && *e ? atoi(e) != 0 : true;
 }
+// K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
+// 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
+// scenes: 2.07 ms for 32,768 waves at 3, 2.29 ms at 4); 262,144 scenes (BASELINE config 5 over 8
+// GPUs) = 4,096 waves = 1.33 rounds at 3 (0.352 ms measured) or exactly 1 at 4. PP_PREP_W4=0/1.
+bool prep_w4(int64_t Sv, int device) {
+    const char* e = getenv("PP_PREP_W4");
+    if (e && *e) return atoi(e) != 0;
+    static int cus[kMaxDev] = {};
+    if (device < 0 || device >= kMaxDev) return false;
+    if (cus[device] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c <= 0) c = 256;
+        cus[device] = c;
+    }
+    const int64_t waves = (Sv + 63) / 64, simds = 4LL * cus[device];
+    const int64_t r3 = (waves + 3 * simds - 1) / (3 * simds), r4 = (waves + 4 * simds - 1) / (4 * simds);
+    return 286 * r4 < 188 * r3;
+}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
@@ -2978,7 +3001,15 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             case 4: { PP_LAUNCH_PREP(k_prep_g4); break; }
             case 8: { PP_LAUNCH_PREP(k_prep_g8); break; }
             case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
-            default: { PP_LAUNCH_PREP(k_prep); break; }
+            default: {
+                if (prep_w4(Sv, device)) {
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb);
+                } else {
+                    PP_LAUNCH_PREP(k_prep);
+                }
+                break;
+            }
         }
 #undef PP_LAUNCH_PREP
     }

@@ -348,7 +348,8 @@ def test_fused_small_invariance(env, case, monkeypatch):
 def test_prep_staged_invariance(env, case, monkeypatch):
     """K1 on large batches stages every car's x, y in LDS (k_prep_st: coalesced row-order loads,
     matching nearest first from LDS, planner pass in row order); PP_PREP_ST=0 forces the gathering
-    k_prep. Both give bit-identical outputs (scene info included) and equal the oracle. Cases:
+    k_prep, and PP_PREP_W4=1 its 4-waves-per-SIMD build (picked for 262,144-scene shards). All give
+    bit-identical outputs (scene info included) and equal the oracle. Cases:
     random scenes; tied duplicate cars with -1, negative and large ids; Monte-Carlo draws (the
     position noise applied where x, y are staged, the velocity noise in the row-order pass)."""
     S = 1500
@@ -367,9 +368,11 @@ def test_prep_staged_invariance(env, case, monkeypatch):
     outs = {}
     try:
         ppamd.set_prep_group(1)          # one lane per evaluation at this size too
-        for f in ("0", "1"):
-            monkeypatch.setenv("PP_PREP_ST", f)
-            outs[f] = run_gpu(env, d, prm, info=case != "draws")
+        # "0": the gathering k_prep (3 waves/SIMD); "1": k_prep_st; "w4": k_prep's 4-wave build
+        for name, st, w4 in (("0", "0", "0"), ("1", "1", "0"), ("w4", "0", "1")):
+            monkeypatch.setenv("PP_PREP_ST", st)
+            monkeypatch.setenv("PP_PREP_W4", w4)
+            outs[name] = run_gpu(env, d, prm, info=case != "draws")
     finally:
         ppamd.set_prep_group(0)
 
@@ -377,8 +380,9 @@ def test_prep_staged_invariance(env, case, monkeypatch):
         if a.dtype.names:
             return all(same(a[f], b[f]) for f in a.dtype.names)
         return np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
-    for k, v in outs["0"].items():
-        assert same(outs["1"][k], v), k
+    for name in ("1", "w4"):
+        for k, v in outs["0"].items():
+            assert same(outs[name][k], v), (name, k)
     if case != "draws":
         ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
         compare(outs["1"], ref)

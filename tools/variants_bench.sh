@@ -12,7 +12,7 @@ for lib in carnd-path-planning-project_amd/ppamd/libppamd.so carnd-path-planning
 import json, sys
 line = [l for l in open("gpurun_out/vb.log") if l.startswith("{")][-1]
 j = json.loads(line)
-print(sys.argv[1].split("/")[-1], "%.4g" % j["value"], j["ms_per_step"], {k: round(v, 3) for k, v in j["kernels_ms_avg"].items()})
+print(sys.argv[1].split("/")[-1], "%.4g" % j["value"], j["ms_per_step"], {k: (round(v, 3) if v is not None else None) for k, v in j["kernels_ms_avg"].items()})
 PY
 done
 cat $out
