@@ -189,7 +189,9 @@ __device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_
 }
 // k_cand groups (SPB scenes per group, or BPS groups per scene): k_prep marks the groups holding a
 // kLimSlow scene in this bitmap for k_cand<true>
-struct GroupBits { uint32_t* bits; int SPB, BPS; };
+// (list/count: the flagged groups in the order k_prep found them, for k_cand<true>; count is zeroed
+// before every K1)
+struct GroupBits { uint32_t* bits; int SPB, BPS; uint32_t* list; uint32_t* count; };
 // ---- K1 building blocks, shared by k_prep (one lane per evaluation) and k_prep_g2..16 (G lanes) ----
 
 // Ego state of one evaluation: derivation (src/main.cpp:1233-1292), Frenet frame and ego matching
@@ -464,7 +466,11 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     if (!ok) lim_mask |= kLimSlow;
     if ((lim_mask & kLimSlow) && r == 0 && gb.bits) {   // (k_step_small: no bitmap)
         const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
-        for (int b = 0; b < gb.BPS; b++) atomicOr(&gb.bits[(g0 + b) >> 5], 1u << ((g0 + b) & 31));
+        for (int b = 0; b < gb.BPS; b++) {
+            const uint32_t bit = 1u << ((g0 + b) & 31);
+            const uint32_t old = atomicOr(&gb.bits[(g0 + b) >> 5], bit);
+            if (!(old & bit) && gb.list) gb.list[atomicAdd(gb.count, 1u)] = (uint32_t)(g0 + b);
+        }
     }
     // the frame's rotations cos(-angle), sin(-angle) (:786-787) and cos(angle), sin(angle)
     // (:822-823) as the reference's libm computes them (pp_glibcm.h): every knot is a product with
@@ -1892,15 +1898,18 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES_PATHS : PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
-                                              uint32_t* gbits, int64_t ngroups) {
+                                              uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
+                                              const uint32_t* gcount) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (!kSlow) {
         cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm);
         return;
     }
-    for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-        const uint32_t word = gbits[g >> 5];                      // same address for every lane
-        if (!((word >> (g & 31)) & 1u)) continue;
+    // the flagged groups k_prep listed (each listed once: the first setter of its bit appends it)
+    const uint32_t nl = *gcount;                                  // same address for every lane
+    for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const int64_t g = glist[i];
+        if (g >= ngroups) continue;                               // (never: k_prep lists this call's groups)
         __syncthreads();                                          // the previous group's LDS readers are done
         cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
@@ -2156,7 +2165,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     {   // K1: scene g SPB + threadIdx.x / 16 by a group of 16 lanes
         const int q = (int)threadIdx.x / 16;
         const int64_t v = g * SPB + q;
-        const GroupBits nobits = {nullptr, SPB, 1};
+        const GroupBits nobits = {nullptr, SPB, 1, nullptr, nullptr};
         if (q < SPB && v < in.n_scenes) prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, v, (int)threadIdx.x % 16);
     }
     __syncthreads();
@@ -2640,13 +2649,16 @@ int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
     return PP_OK;
 }
 
+// The slow-group bitmap (words), then the flagged-group count and list (ngroups entries), in one
+// allocation: [cap words][count][list: 32 cap entries]
 int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     const int64_t words = (ngroups + 31) / 32;
     if (W.gbits_cap >= words) return PP_OK;
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
-    if (hipMalloc(&W.gbits, sizeof(uint32_t) * cap) != hipSuccess) return PP_ERR_NOMEM;
-    if (hipMemsetAsync(W.gbits, 0, sizeof(uint32_t) * cap, st) != hipSuccess) return PP_ERR_HIP;
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 1 + 32 * cap);
+    if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
     return PP_OK;
 }
@@ -2944,6 +2956,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
+    gb.count = W.gbits + W.gbits_cap;
+    gb.list = gb.count + 1;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -2971,6 +2985,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
+    if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
         const int threads = 256;
@@ -3021,9 +3036,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (timing) (void)hipEventRecord(ev[1], st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng);                                         \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count);                      \
         hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng)
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count)
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
         else if (ref_direct && fused) {
             hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
