@@ -132,8 +132,11 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #ifndef PP_TEAM_SETUP
 #define PP_TEAM_SETUP 1
 #endif
+#ifndef PP_WIN_INLINE          // reference mode: winner lanes write next_x/next_y in k_cand (no k_emit)
+#define PP_WIN_INLINE 0
+#endif
 #ifndef PP_SEG_MODE
-#define PP_SEG_MODE 0
+#define PP_SEG_MODE 3
 #endif
 // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
 #ifndef PP_WALK_PF
@@ -528,7 +531,8 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
 // whole rounds of 4 waves per SIMD better than of 3 (prep_w4 in pp_eval)
 template <bool kLdsMap, bool kW4 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
-                                              pp_scene_info* info, uint32_t* out_status, GroupBits gb) {
+                                              pp_scene_info* info, uint32_t* out_status, GroupBits gb,
+                                              int64_t v0, int64_t v1) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
     if (kLdsMap) {
@@ -541,8 +545,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
     const int64_t S = in.n_scenes;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int64_t Sv = S * D;
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= Sv) return;
+    // evaluations [v0, v1) of the batch (pp_eval's chunked pipeline launches K1 per chunk)
+    const int64_t v = v0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= v1 || v >= Sv) return;
     const int64_t s = D == 1 ? v : v / D;
     const int draw = (int)(v - s * D);
 
@@ -1260,9 +1265,14 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         R.ng = ng;
         return R;
     }
-    int cnt = 0;                     // #knots with X < x (std::lower_bound position)
     // cached segment: valid while seg_lo < x <= seg_hi (NaN x never valid)
+#if PP_SEG_MODE == 3
+    int cnt = -1;                    // #knots with X < x (std::lower_bound position); -1: none yet
+    double seg_lo = 1.0, seg_hi = -__builtin_inf(), sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
+#else
+    int cnt = 0;                     // #knots with X < x (std::lower_bound position)
     double seg_lo = 1.0, seg_hi = 0.0, sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
+#endif
     double arg = 0, prev_speed = sc.start;
 #if PP_ANGLE_CROSS
     double uxp = 1.0, uyp = 0.0;     // previous step direction (angle 0: the local frame's x axis)
@@ -1309,7 +1319,35 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             && ng == 0
 #endif
         ) {
-#if PP_SEG_MODE == 1      // forward only unless x fell below the cached segment
+#if PP_SEG_MODE == 3
+            // forward miss (x passed the cached segment's end; the first step starts from cnt = -1,
+            // seg_hi = -inf): x(cnt) = seg_hi < x is known, so the walk resumes one knot further
+            // and the bounds come from the walk's own reads — one LDS round trip for the knot and
+            // one for the coefficients, instead of the two loops' re-reads
+            if (__builtin_expect(x > seg_hi, 1)) {
+                double xlo = seg_hi, xhi;
+                cnt++;
+                for (;;) {
+                    xhi = cnt < nk ? sl.x(cnt) : __builtin_inf();
+                    if (!(xhi < x)) break;
+                    xlo = xhi;
+                    cnt++;
+                }
+                seg_lo = xlo;
+                seg_hi = xhi;
+                const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+                sx = cnt > 0 ? xlo : xhi;
+                sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+            } else {
+                if (cnt < 0) cnt = 0;
+                while (cnt < nk && sl.x(cnt) < x) cnt++;
+                while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
+                const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+                seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
+                seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
+                sx = sl.x(idx); sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+            }
+#elif PP_SEG_MODE == 1    // forward only unless x fell below the cached segment
             if (__builtin_expect(x <= seg_lo, 0)) while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
             else while (cnt < nk && sl.x(cnt) < x) cnt++;
 #else
@@ -1317,10 +1355,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
 #endif
             PP_DIAGC(1, true);
+#if PP_SEG_MODE != 3
             const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
             seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
             seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
             sx = sl.x(idx); sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+#endif
         }
 #endif
         const double h = x - sx;
@@ -1824,10 +1864,37 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 out.winner[s] = c;
             }
 #ifdef PP_ABL_NO_REC       // diagnostic timing build: the first wave runs the cost-only loop too
-        } else if (false) {
+#define PP_REC_WAVE false
 #else
-        } else if (kMode == 1 && tid < 64) {
+#define PP_REC_WAVE (kMode == 1 && tid < 64)
 #endif
+        } else if (PP_REC_WAVE && PP_WIN_INLINE && !emit_in) {
+            // reference mode, the block's first wave: the winners transform their path as they
+            // walk it and write next_x/next_y (the kept previous points first, zeros after the
+            // last point); the other lanes of the wave are cost-only
+            double* wx = nullptr;
+            double* wy = nullptr;
+            if (winner) {
+                for (int i = 0; i < K; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 9)) break;
+                    out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+                    out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+                }
+                wx = out.next_x + (int64_t)K * S + s;
+                wy = out.next_y + (int64_t)K * S + s;
+            }
+            R = run_candidate<kSlow, 1, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
+                                                       pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
+                                                       nullptr, 0, winner);
+            if (winner) {
+                for (int i = K + R.ng; i < N; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 10)) break;
+                    out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0;
+                }
+                out.n_out[s] = K + R.ng;
+                out.winner[s] = c;
+            }
+        } else if (PP_REC_WAVE) {
             // reference mode, the block's first wave: the winners record their local path
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
             R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
@@ -1899,10 +1966,10 @@ template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES_PATHS : PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
                                               uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
-                                              const uint32_t* gcount) {
+                                              const uint32_t* gcount, int64_t g0) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (!kSlow) {
-        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, blockIdx.x, sm);
+        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g0 + blockIdx.x, sm);
         return;
     }
     // the flagged groups k_prep listed (each listed once: the first setter of its bit appends it)
@@ -2119,9 +2186,9 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
 
 template <int kChunk>
 __global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
-                                              const double* rec, const uint64_t* adjm) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= in.n_scenes) return;
+                                              const double* rec, const uint64_t* adjm, int64_t s0, int64_t s1) {
+    const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // scenes [s0, s1)
+    if (s >= s1 || s >= in.n_scenes) return;
     emit_scene<kChunk>(in, P, pv, out, rec, adjm, s);
 }
 
@@ -2373,6 +2440,8 @@ struct StreamWS {
     int64_t rec_cap = 0;
     uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
     int64_t gbits_cap = 0;        // words
+    hipStream_t aux = nullptr;    // the chunked pipeline's second stream (K1 and K4 of other chunks)
+    std::vector<hipEvent_t> sev;  // its synchronisation events
 };
 struct DevState {
     bool init = false;
@@ -2605,6 +2674,20 @@ bool prep_w4(int64_t Sv, int device) {
     const int64_t r3 = (waves + 3 * simds - 1) / (3 * simds), r4 = (waves + 4 * simds - 1) / (4 * simds);
     return 286 * r4 < 188 * r3;
 }
+// pp_eval's two-stream pipeline: chunks of the k_cand groups for batches of at least kPipeMin scenes
+// (PP_CHUNKS=n forces n chunks, 1 = off; at most kMaxChunks, and at least 64 groups per chunk)
+constexpr int64_t kPipeMin = 131072;
+constexpr int kMaxChunks = 16;
+#ifndef PP_PIPE_CHUNKS
+#define PP_PIPE_CHUNKS 1
+#endif
+int pipe_chunks(int64_t S, int64_t groups) {
+    const char* e = getenv("PP_CHUNKS");
+    int n = e && *e ? atoi(e) : (S >= kPipeMin ? PP_PIPE_CHUNKS : 1);
+    if (n > kMaxChunks) n = kMaxChunks;
+    while (n > 1 && groups < 64LL * n) n--;
+    return n < 1 ? 1 : n;
+}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
 std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
@@ -2649,14 +2732,15 @@ int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
     return PP_OK;
 }
 
-// The slow-group bitmap (words), then the flagged-group count and list (ngroups entries), in one
-// allocation: [cap words][count][list: 32 cap entries]
+// The slow-group bitmap (words), then the flagged-group counts (one per pipeline chunk) and list
+// (ngroups entries; chunk c's entries from its first group on), in one allocation:
+// [cap words][kMaxChunks counts][list: 32 cap entries]
 int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     const int64_t words = (ngroups + 31) / 32;
     if (W.gbits_cap >= words) return PP_OK;
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
-    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 1 + 32 * cap);
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + kMaxChunks + 32 * cap);
     if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
@@ -2667,7 +2751,20 @@ void free_ws(StreamWS& W) {
     if (W.ws) (void)hipFree(W.ws);
     if (W.rec) (void)hipFree(W.rec);
     if (W.gbits) (void)hipFree(W.gbits);
+    for (hipEvent_t e : W.sev) (void)hipEventDestroy(e);
+    if (W.aux) (void)hipStreamDestroy(W.aux);
     W = StreamWS();
+}
+
+// the chunked pipeline's stream and at least n synchronisation events (callers hold M->mu)
+int ensure_aux(StreamWS& W, size_t n) {
+    if (!W.aux && hipStreamCreateWithFlags(&W.aux, hipStreamNonBlocking) != hipSuccess) { W.aux = nullptr; return PP_ERR_HIP; }
+    while (W.sev.size() < n) {
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
+        W.sev.push_back(e);
+    }
+    return PP_OK;
 }
 
 // k_cand's launch geometry for C candidates per scene (BPS == 1: SPB scenes per group; else one
@@ -2957,7 +3054,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     gb.count = W.gbits + W.gbits_cap;
-    gb.list = gb.count + 1;
+    gb.list = gb.count + kMaxChunks;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -2982,6 +3079,71 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(cg.threads), lds_f, st, mg, B, P, pv,
                            R, spb_f, rec, adjm);
         if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
+        if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+        return PP_OK;
+    }
+    // Large reference-mode batches: a two-stream pipeline over chunks of the k_cand groups. The
+    // caller's stream runs only K2 (chunk after chunk); the second stream runs K1 of chunk c + 1
+    // and K4 of chunk c - 1 meanwhile, so the latency-bound K1 and the memory-bound K4 fill what
+    // the VALU-bound K2 leaves idle. Same kernels, same arithmetic, per-chunk
+    // ranges: the results are those of the one-chunk launch, bit for bit (tests/test_pipeline.py).
+    const int nch = pipe_chunks(S, cg.groups);
+    if (nch > 1 && ref_direct && !P.emit_paths && cg.bps == 1 && Dn == 1 && prep_group(Sv) == 1 &&
+        !prep_st_on() && !PP_WIN_INLINE) {
+        rc = ensure_aux(W, 2 * (size_t)nch + 2);
+        if (rc) return rc;
+        hipStream_t ax = W.aux;
+        hipEvent_t* pe = W.sev.data();               // pe[c]: K1 of chunk c done
+        hipEvent_t* ce = pe + nch;                   // ce[c]: K2 of chunk c done
+        hipEvent_t e_start = W.sev[2 * nch], e_done = W.sev[2 * nch + 1];
+        const bool lmap = mg.n <= kLdsMapMax;
+        const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
+        int64_t gstep = (cg.groups + nch - 1) / nch;
+        gstep = (gstep + 63) / 64 * 64;              // chunk boundaries on 64-group (32-bit word, 64-scene-multiple) edges
+        auto g_lo = [&](int c) { return std::min<int64_t>((int64_t)c * gstep, cg.groups); };
+        auto s_lo = [&](int c) { return std::min<int64_t>(g_lo(c) * cg.spb, S); };
+        auto prep = [&](int c) {
+            GroupBits gc = gb;
+            gc.count = gb.count + c;
+            gc.list = gb.list + g_lo(c);
+            const int64_t v0 = s_lo(c), v1 = s_lo(c + 1);
+            if (v1 <= v0) return;
+            const unsigned blocks = (unsigned)((v1 - v0 + 255) / 256);
+            if (prep_w4(v1 - v0, device)) {
+                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(blocks), dim3(256), lds, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, true>), dim3(blocks), dim3(256), 0, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+            } else {
+                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(blocks), dim3(256), lds, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, false>), dim3(blocks), dim3(256), 0, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+            }
+        };
+        auto emit = [&](int c) {
+            const int64_t s0 = s_lo(c), s1 = s_lo(c + 1);
+            if (s1 <= s0) return;
+            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)((s1 - s0 + 255) / 256)), dim3(256), 0, ax, B, P,
+                               pv, R, rec, adjm, s0, s1);
+        };
+        if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t) * nch, st) != hipSuccess) return PP_ERR_HIP;
+        if (timing) (void)hipEventRecord(ev[0], st);
+        if (hipEventRecord(e_start, st) != hipSuccess || hipStreamWaitEvent(ax, e_start, 0) != hipSuccess) return PP_ERR_HIP;
+        for (int c = 0; c < 2 && c < nch; c++) { prep(c); if (hipEventRecord(pe[c], ax) != hipSuccess) return PP_ERR_HIP; }
+        for (int c = 0; c < nch; c++) {
+            if (hipStreamWaitEvent(st, pe[c], 0) != hipSuccess) return PP_ERR_HIP;
+            if (c == 0 && timing) (void)hipEventRecord(ev[1], st);
+            const int64_t g0 = g_lo(c), g1 = g_lo(c + 1);
+            if (g1 > g0) {
+                hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
+                                   cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
+                hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)std::min<int64_t>(g1 - g0, 2048)), dim3(cg.threads), cg.lds, st,
+                                   mg, B, P, pv, R, cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
+            }
+            if (hipEventRecord(ce[c], st) != hipSuccess || hipStreamWaitEvent(ax, ce[c], 0) != hipSuccess) return PP_ERR_HIP;
+            emit(c);
+            if (c + 2 < nch) { prep(c + 2); if (hipEventRecord(pe[c + 2], ax) != hipSuccess) return PP_ERR_HIP; }
+        }
+        if (timing) (void)hipEventRecord(ev[2], st);
+        if (hipEventRecord(e_done, ax) != hipSuccess || hipStreamWaitEvent(st, e_done, 0) != hipSuccess) return PP_ERR_HIP;
+        if (timing) (void)hipEventRecord(ev[3], st);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
@@ -3018,10 +3180,11 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
             default: {
                 if (prep_w4(Sv, device)) {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb);
-                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 } else {
-                    PP_LAUNCH_PREP(k_prep);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 }
                 break;
             }
@@ -3036,9 +3199,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (timing) (void)hipEventRecord(ev[1], st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count);                      \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0);          \
         hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count)
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0)
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
         else if (ref_direct && fused) {
             hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
@@ -3050,13 +3213,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
-    if (ref_direct && !P.emit_paths && !emit_in) {
+    if (ref_direct && !P.emit_paths && !emit_in && !PP_WIN_INLINE) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
             const int64_t blocks = (S + 63) / 64;
-            hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm);
+            hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         } else {
             const int64_t blocks = (S + 255) / 256;
-            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm);
+            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         }
     }
     // K3 (comfort mode, or any mode with draws): argmin + winner path

@@ -1,9 +1,9 @@
 set -o pipefail
-O=gpurun_out/r02ac; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
-tail -1 $O/gpu_tests.log
-timeout -k 10 120 python bench.py --no-cpu-baseline --steps 20 > $O/c5.json 2> $O/c5.err || exit 1
-python -c "import json;j=json.loads(open('$O/c5.json').read().strip().splitlines()[-1]);print('c5',j['ms_per_step'],j['value']/1e9,j['kernels_ms_avg'])"
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$O/stats -o run -- python3 bench.py --no-cpu-baseline > $O/c5_prof.json 2> $O/c5_prof.err || exit 1
-cut -c1-120 $O/stats/run_kernel_stats.csv | head -8
+O=gpurun_out/${1:-var}; mkdir -p $O
+export TMPDIR=/tmp
+ROOT=$PWD
+for v in base nocars nomatch; do
+  if [ $v = base ]; then L=$ROOT/carnd-path-planning-project_amd/ppamd/libppamd.so; else L=$ROOT/carnd-path-planning-project_amd/ppamd/libppamd_var_$v.so; fi
+  PPAMD_LIB=$L timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $ROOT/$O/$v -o $v -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/$v.log 2>&1 || { tail $O/$v.log; exit 1; }
+  echo "$v done"
+done
