@@ -339,12 +339,153 @@ __device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double
     return found;
 }
 
+// lane_matching_tab with lighter bookkeeping (same walk, same arithmetic, same results):
+// - the walk is monotone (a direction change stops it, :237-246), so a segment's end points are
+//   carried to the next iteration (forward: b becomes a; backward: a becomes b) and only the new
+//   point is loaded;
+// - an improvement records only its lane (and the best distance); the iteration's segment, the
+//   lane's running sum_s and ratio shift are kept once per improving iteration, and the recorded
+//   projection's rnom/snom are recomputed after the walk by the same operations.
+#ifndef PP_MATCH_CARRY      // carry the segment's end points across iterations (register pressure)
+#define PP_MATCH_CARRY 0
+#endif
+__device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const double ratio[NL], double x,
+                                          double y, double& out_s, double& out_d, int& out_lane,
+                                          int& out_next_wp) {
+    const int n = m.n;
+    int dir = 0;
+    bool stop = false;
+    int cur = ref_wp;
+    int a = wpi(cur - 1, n), b = wpi(cur, n);
+    double sum_s[NL], sr[NL];
+#pragma unroll
+    for (int l = 0; l < NL; l++) { sum_s[l] = 0; sr[l] = ratio[l]; }
+#if PP_MATCH_CARRY
+    double ax[NL], ay[NL], bx[NL], by[NL];
+#pragma unroll
+    for (int l = 0; l < NL; l++) {
+        ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a];
+        bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b];
+    }
+#endif
+    double best = 1000 * 1000;
+    bool found = false;
+    int b_lane = 0, k_cur = 0, k_b = 0, k_a = 0;
+    double k_ss = 0, k_sr = 0;
+    for (int it = 0; it < 4 * n + 8; it++) {
+        PP_DIAGC(16, true);
+        bool improved = false;
+        int il = 0;
+#pragma unroll
+        for (int lane = 0; lane < NL; lane++) {
+#if PP_MATCH_CARRY
+            const double pax = ax[lane], pay = ay[lane], pbx = bx[lane], pby = by[lane];
+#else
+            const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
+            const double pbx = m.lc_x[lane * n + b], pby = m.lc_y[lane * n + b];
+#endif
+            const double den = m.lden[lane * n + b];
+            const double pdx = x - pax, dx = pbx - pax;                        // helpers.h:203-207
+            const double pdy = y - pay, dy = pby - pay;
+            const double rn = pdx * dx + pdy * dy;
+            double rnom, dsq;
+            if (rn < -1) { rnom = 0; dsq = pdx * pdx + pdy * pdy; }                                       // :227-231
+            else if (rn > den) { rnom = den; dsq = (x - pbx) * (x - pbx) + (y - pby) * (y - pby); }       // :232-236
+            else {
+                const double snom = pdx * dy - pdy * dx;
+                rnom = rn; dsq = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]);
+            }
+            if (dsq < best) { best = dsq; improved = true; il = lane; }
+            if (rnom == 0) {
+                if (dir == 1) stop = true;
+                dir = -1;
+            } else if (rnom == den) {
+                if (dir == -1) stop = true;
+                dir = 1;
+            } else {
+                stop = true;
+            }
+        }
+        if (improved) {          // this iteration holds the last improvement so far
+            found = true;
+            b_lane = il; k_cur = cur; k_a = a; k_b = b;
+            k_ss = sum_s[0]; k_sr = sr[0];
+#pragma unroll
+            for (int l = 1; l < NL; l++) if (il == l) { k_ss = sum_s[l]; k_sr = sr[l]; }
+        }
+        if (!improved || stop) break;
+        if (dir > 0) {
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] += (1 - sr[l]) * m.llen[l * n + b]; sr[l] = 0; }
+            cur++;
+            a = b;
+            b = b + 1 == n ? 0 : b + 1;
+#if PP_MATCH_CARRY
+            if (__builtin_expect(cur - 1 < -n, 0)) {
+                a = wpi(cur - 1, n); b = wpi(cur, n);
+#pragma unroll
+                for (int l = 0; l < NL; l++) { ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a]; }
+            } else {
+#pragma unroll
+                for (int l = 0; l < NL; l++) { ax[l] = bx[l]; ay[l] = by[l]; }
+            }
+#pragma unroll
+            for (int l = 0; l < NL; l++) { bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b]; }
+#else
+            if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
+#endif
+        } else {
+#pragma unroll
+            for (int l = 0; l < NL; l++) { sum_s[l] -= sr[l] * m.llen[l * n + b]; sr[l] = 1; }
+            cur--;
+            b = a;
+            a = a == 0 ? n - 1 : a - 1;
+#if PP_MATCH_CARRY
+            if (__builtin_expect(cur - 1 < -n, 0)) {
+                a = wpi(cur - 1, n); b = wpi(cur, n);
+#pragma unroll
+                for (int l = 0; l < NL; l++) { bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b]; }
+            } else {
+#pragma unroll
+                for (int l = 0; l < NL; l++) { bx[l] = ax[l]; by[l] = ay[l]; }
+            }
+#pragma unroll
+            for (int l = 0; l < NL; l++) { ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a]; }
+#else
+            if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
+#endif
+        }
+    }
+    if (found) {                                                   // :214-227, last improvement
+        const int l = b_lane;
+        const double pax = m.lc_x[l * n + k_a], pay = m.lc_y[l * n + k_a];
+        const double pbx = m.lc_x[l * n + k_b], pby = m.lc_y[l * n + k_b];
+        const double den = m.lden[l * n + k_b];
+        const double pdx = x - pax, dx = pbx - pax;
+        const double pdy = y - pay, dy = pby - pay;
+        const double rn = pdx * dx + pdy * dy;
+        const double snom = pdx * dy - pdy * dx;
+        const double rnom = rn < -1 ? 0.0 : (rn > den ? den : rn);
+        const double rfs = rnom / den;
+        const double r_mod = rfs - k_sr;
+        const double seg_len = m.llen[l * n + k_b];
+        out_s = k_ss + seg_len * r_mod;
+        double d = sqrt(best);
+        if (snom < 0) d = -d;
+        out_d = d + lane_offset(l);
+        out_lane = l;
+        out_next_wp = k_cur;
+    }
+    return found;
+}
+
 __device__ __forceinline__ bool lane_match(const MapV& m, int ref_wp, const double ratio[NL], double x,
                                            double y, double& out_s, double& out_d, int& out_lane,
                                            int& out_next_wp) {
 #ifndef PP_MATCH_TAB
-#define PP_MATCH_TAB 1
+#define PP_MATCH_TAB 2
 #endif
+    if (PP_MATCH_TAB == 2 && m.fastm) return lane_matching_tab2(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
     if (PP_MATCH_TAB && m.fastm) return lane_matching_tab(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
     return lane_matching(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
 }

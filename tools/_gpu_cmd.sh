@@ -1,9 +1,9 @@
 set -o pipefail
 O=gpurun_out/${1:-var}; mkdir -p $O
 export TMPDIR=/tmp
-ROOT=$PWD
-for v in base nocars nomatch; do
-  if [ $v = base ]; then L=$ROOT/carnd-path-planning-project_amd/ppamd/libppamd.so; else L=$ROOT/carnd-path-planning-project_amd/ppamd/libppamd_var_$v.so; fi
-  PPAMD_LIB=$L timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $ROOT/$O/$v -o $v -- python3 $ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/$v.log 2>&1 || { tail $O/$v.log; exit 1; }
-  echo "$v done"
-done
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+PPAMD_LIB=$PWD/carnd-path-planning-project_amd/ppamd/libppamd_var_carry.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_baseline_configs.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/carry_tests.log 2>&1 || { tail -30 $O/carry_tests.log; exit 1; }
+tail -1 $O/carry_tests.log
+bash tools/variants_bench.sh --steps 20 || exit 1
+cp gpurun_out/variants.txt $O/
