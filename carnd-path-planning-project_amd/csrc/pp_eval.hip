@@ -1550,7 +1550,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         pos_y += (y - pos_y) * dstep / d;
 #endif
         arg += sp_step;
-        pos_x += sp_step;
+        pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
         if (kOutMode != 0 && kOut) {
             const double tx = pos_x * ca - pos_y * sa;
             const double ty = pos_x * sa + pos_y * ca;
@@ -2185,7 +2185,10 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
 }
 
 template <int kChunk>
-__global__ __launch_bounds__(256) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+#ifndef PP_EMIT_WAVES            // k_emit occupancy (waves per SIMD); 0: the compiler's choice
+#define PP_EMIT_WAVES 0
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_EMIT_WAVES > 0 ? PP_EMIT_WAVES : 1))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                               const double* rec, const uint64_t* adjm, int64_t s0, int64_t s1) {
     const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // scenes [s0, s1)
     if (s >= s1 || s >= in.n_scenes) return;
