@@ -19,7 +19,11 @@ namespace ppd {
 
 constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
 constexpr double kEps = 1e-5;                     // src/main.cpp:24
-constexpr int kKP = 17;                           // LDS knot stride (16 knots + 1 pad: bank spread)
+#ifndef PP_KKP
+#define PP_KKP 17
+#endif
+constexpr int kKP = PP_KKP;                       // LDS knot stride (16 knots + 1 pad: bank spread)
+static_assert(kKP >= 15, "a slot holds npk + ncp <= (PP_PREV_KEEP - 1) + 6 = 15 knots");
 constexpr int NL = PP_NUM_LANES;                  // lanes (src/main.cpp:22)
 // ref x/y, normal x/y, lane centre x[NL]/y[NL], length[NL], segment |.|^2 [NL] and its reciprocal [NL]
 constexpr int kMapArrays = 4 + 5 * NL;
@@ -477,6 +481,69 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
         out_next_wp = k_cur;
     }
     return found;
+}
+
+// ---- lane_matching in two passes (k_prep's flattened car loop) ----
+// Pass 1 only walks: per car it keeps the walk's outcome (found, lane and segment of the last
+// improvement) in a 16-bit word. Pass 2 rebuilds s and d of that projection by the walk's own
+// operations: the distance and the projection terms of the recorded (lane, segment), and the
+// lane's running sum_s over the segments from ref_wp to that segment (the walk is monotone, so the
+// ratio shift is ratio[lane] at ref_wp, 0 after forward steps, 1 after backward ones: :255-272).
+// Same values as lane_matching_tab2, bit for bit.
+// word: bit 15 found, bits 12-14 lane, bits 0-11 (segment - ref_wp) + 2048; kWalkRedo: the
+// segment lies beyond that range (pass 2 runs lane_matching_tab2 itself); 0: no projection.
+constexpr uint16_t kWalkRedo = 0x7000;
+
+// one lane segment's squared distance and clamped projection (helpers.h:188-249 with the tables;
+// the same operations as lane_matching_tab2's walk)
+__device__ __forceinline__ double seg_dsq(const MapV& m, int lane, int a, int b, double x, double y,
+                                          double& rnom, double& snom, double& den) {
+    const int n = m.n;
+    const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
+    const double pbx = m.lc_x[lane * n + b], pby = m.lc_y[lane * n + b];
+    den = m.lden[lane * n + b];
+    const double pdx = x - pax, dx = pbx - pax;
+    const double pdy = y - pay, dy = pby - pay;
+    const double rn = pdx * dx + pdy * dy;
+    snom = pdx * dy - pdy * dx;
+    if (rn < -1) { rnom = 0; return pdx * pdx + pdy * pdy; }
+    if (rn > den) { rnom = den; return (x - pbx) * (x - pbx) + (y - pby) * (y - pby); }
+    rnom = rn;
+    return div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]);
+}
+
+// pass 2: s, d, lane and next waypoint of the projection a pass-1 word records (found bit set)
+__device__ __forceinline__ void walk_finish(const MapV& m, int ref_wp, const double ratio[NL], double x,
+                                            double y, uint32_t w, double& out_s, double& out_d,
+                                            int& out_lane, int& out_next_wp) {
+    const int n = m.n;
+    const int l = (int)((w >> 12) & 7);
+    const int kc = ref_wp + (int)(w & 0xFFF) - 2048;
+    // the lane's running sum_s and ratio shift when the walk stood at segment kc (:255-272)
+    double sr = ratio[0];
+    asm("" : "+v"(sr));                       // a select chain, not an indexed (scratch) load
+#pragma unroll
+    for (int i = 1; i < NL; i++) {
+        double ri = ratio[i];
+        asm("" : "+v"(ri));
+        sr = l == i ? ri : sr;
+    }
+    double ss = 0;
+    if (kc > ref_wp) {
+        for (int c = ref_wp; c < kc; c++) { ss += (1 - sr) * m.llen[l * n + wpi(c, n)]; sr = 0; }
+    } else if (kc < ref_wp) {
+        for (int c = ref_wp; c > kc; c--) { ss -= sr * m.llen[l * n + wpi(c, n)]; sr = 1; }
+    }
+    const int b = wpi(kc, n), a = wpi(kc - 1, n);
+    double rnom, snom, den;
+    const double dsq = seg_dsq(m, l, a, b, x, y, rnom, snom, den);
+    const double r_mod = rnom / den - sr;
+    out_s = ss + m.llen[l * n + b] * r_mod;
+    double d = sqrt(dsq);
+    if (snom < 0) d = -d;
+    out_d = d + lane_offset(l);
+    out_lane = l;
+    out_next_wp = kc;
 }
 
 __device__ __forceinline__ bool lane_match(const MapV& m, int ref_wp, const double ratio[NL], double x,

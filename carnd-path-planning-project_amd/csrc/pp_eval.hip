@@ -527,6 +527,91 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
     cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
 }
 
+// K1's car pass without a car table and without Monte-Carlo draws: lane_matching in two passes
+// (pp_device.h, walk_finish). Pass 1 runs all of a lane's car walks as one flat loop — a lane whose
+// walk ends takes its next car in the same iteration — so the lanes of a wave stay busy until their
+// own total walk length is spent, instead of idling at every car until the wave's longest walk for
+// that car ends. Each walk's outcome is a 16-bit word in LDS (kFlatCars cars per round). Pass 2
+// visits the cars in row order (the reference's own order, src/main.cpp:1325-1411; coalesced
+// reads), rebuilds each projection from its word and feeds the planner.
+// Measured and kept opt-in (PP_PREP_FLAT=1; bit-identical, the GPU suite passes with it): at 3
+// waves/SIMD k_prep 2.07 -> 2.23 ms on the config-5 batch. A lane that finishes a walk loads its
+// next car's position while the others walk on; the wave's next read of that register waits for
+// the most recent of those loads, so nearly every iteration pays a memory latency.
+#ifndef PP_PREP_FLAT
+#define PP_PREP_FLAT 0
+#endif
+constexpr int kFlatCars = 16;
+constexpr size_t kFlatLds = sizeof(uint16_t) * kFlatCars * 256;   // per 256-lane block
+constexpr size_t kPrepLdsFlat = PP_PREP_FLAT ? kFlatLds : 0;       // k_prep's dynamic LDS after the map
+
+__device__ __forceinline__ void prep_cars_flat(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                               int64_t S, int64_t s, const EgoSt& e, int T_in, int iters,
+                                               uint16_t* res, PlanAcc& acc, uint32_t& status) {
+    const int n = m.n;
+    const int wmax = 4 * n + 8;                       // lane_matching's bound (never reached)
+    const int a0 = wpi(e.ref_wp - 1, n), b0 = wpi(e.ref_wp, n);
+    for (int c0 = 0; c0 < iters; c0 += kFlatCars) {
+        const int c1 = iters - c0 < kFlatCars ? iters : c0 + kFlatCars;
+        // pass 1: the walks of cars [c0, c1), the next car's position loaded one walk ahead
+        int j = c0;
+        double x = in.car_x[(int64_t)j * S + s], y = in.car_y[(int64_t)j * S + s];
+        double nx = 0, ny = 0;
+        if (j + 1 < c1) { nx = in.car_x[(int64_t)(j + 1) * S + s]; ny = in.car_y[(int64_t)(j + 1) * S + s]; }
+        int cur = e.ref_wp, a = a0, b = b0, dir = 0, itc = 0, kc = 0, kl = 0;
+        bool found = false;
+        double best = 1000 * 1000;
+        for (;;) {
+            PP_DIAGC(16, true);
+            bool improved = false, stop = false;
+            int il = 0;
+#pragma unroll
+            for (int l = 0; l < NL; l++) {                           // src/main.cpp:215-252
+                double rnom, snom, den;
+                const double dsq = seg_dsq(m, l, a, b, x, y, rnom, snom, den);
+                if (dsq < best) { best = dsq; improved = true; il = l; }
+                if (rnom == 0) { if (dir == 1) stop = true; dir = -1; }
+                else if (rnom == den) { if (dir == -1) stop = true; dir = 1; }
+                else stop = true;
+            }
+            if (improved) { found = true; kc = cur; kl = il; }
+            if (improved && !stop && ++itc < wmax) {                 // :253-272
+                if (dir > 0) { cur++; a = b; b = b + 1 == n ? 0 : b + 1; }
+                else { cur--; b = a; a = a == 0 ? n - 1 : a - 1; }
+                if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
+                continue;
+            }
+            uint16_t w = 0;
+            if (found) {
+                const int off = kc - e.ref_wp;
+                w = off >= -2048 && off <= 2047 ? (uint16_t)(0x8000 | (kl << 12) | (off + 2048)) : kWalkRedo;
+            }
+            res[(j - c0) * 256] = w;
+            if (++j >= c1) break;
+            x = nx; y = ny;
+            if (j + 1 < c1) { nx = in.car_x[(int64_t)(j + 1) * S + s]; ny = in.car_y[(int64_t)(j + 1) * S + s]; }
+            cur = e.ref_wp; a = a0; b = b0; dir = 0; itc = 0; found = false; best = 1000 * 1000;
+        }
+        // pass 2: row order; the projection each walk recorded, then project_speed and the planner
+        for (int r = c0; r < c1; r++) {
+            const int64_t ix = (int64_t)r * S + s;
+            const uint32_t w = res[(r - c0) * 256];
+            const double cx = in.car_x[ix], cy = in.car_y[ix];
+            double cs, cd;
+            int clane = 0, nwp = 0;
+            if (w & 0x8000) {
+                walk_finish(m, e.ref_wp, e.ratio, cx, cy, w, cs, cd, clane, nwp);
+            } else if (w != kWalkRedo || !lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
+                status |= PP_ST_CAR_UNMATCHED;                       // :1336-1341
+                continue;
+            }
+            double cvs, cvd;
+            project_speed(m, in.car_vx[ix], in.car_vy[ix], nwp, cvs, cvd);
+            acc.add(P, e, T_in, r, in.car_id[ix], cs, cd, clane, cvs, cvd);
+        }
+    }
+}
+
 // kW4: the 4-waves-per-SIMD instantiation (<= 128 VGPRs): for batches whose wave count fills
 // whole rounds of 4 waves per SIMD better than of 3 (prep_w4 in pp_eval)
 template <bool kLdsMap, bool kW4 = false>
@@ -568,6 +653,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
     const int iters = 0;
 #else
     const int iters = tab ? in.tab_slots : ncar;
+#endif
+#if PP_PREP_FLAT
+    if (!tab && D == 1 && m.fastm) {      // (block-uniform) the flattened two-pass car loop
+        uint16_t* res = (uint16_t*)(smap + (kLdsMap ? kMapArrays * n : 0)) + threadIdx.x;
+        prep_cars_flat(m, in, P, S, s, e, T_in, iters, res, a, status);
+        prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
+        return;
+    }
 #endif
     // Visiting order (PlanAcc: any order once ties compare the iteration index). Without a car
     // table the rows are visited nearest first (squared distance to the ego, a 4-bit row index in
@@ -2711,6 +2804,17 @@ int prep_group(int64_t Sv) {
     return G;
 }
 
+// k_prep's dynamic LDS (map + the flattened car pass's words) may pass 64 KB (maps of 400+
+// waypoints): allow one workgroup the whole 160 KB, once per process
+void prep_lds_attr() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const void* f[4] = {(const void*)k_prep<true, false>, (const void*)k_prep<true, true>,
+                            (const void*)k_prep<false, false>, (const void*)k_prep<false, true>};
+        for (const void* k : f) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMaxBlock);
+    });
+}
+
 int cands_per_block(int C) {
     int spb = 256 / C;
     if (spb > 64 / NL) spb = 64 / NL;      // <= 64 LDS spline slots per workgroup
@@ -3105,6 +3209,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         gstep = (gstep + 63) / 64 * 64;              // chunk boundaries on 64-group (32-bit word, 64-scene-multiple) edges
         auto g_lo = [&](int c) { return std::min<int64_t>((int64_t)c * gstep, cg.groups); };
         auto s_lo = [&](int c) { return std::min<int64_t>(g_lo(c) * cg.spb, S); };
+        prep_lds_attr();
         auto prep = [&](int c) {
             GroupBits gc = gb;
             gc.count = gb.count + c;
@@ -3113,11 +3218,11 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             if (v1 <= v0) return;
             const unsigned blocks = (unsigned)((v1 - v0 + 255) / 256);
             if (prep_w4(v1 - v0, device)) {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(blocks), dim3(256), lds, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, true>), dim3(blocks), dim3(256), 0, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(blocks), dim3(256), lds + kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, true>), dim3(blocks), dim3(256), kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
             } else {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(blocks), dim3(256), lds, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, false>), dim3(blocks), dim3(256), 0, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(blocks), dim3(256), lds + kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, false>), dim3(blocks), dim3(256), kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
             }
         };
         auto emit = [&](int c) {
@@ -3150,6 +3255,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
+    prep_lds_attr();
     if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
@@ -3183,11 +3289,11 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
             default: {
                 if (prep_w4(Sv, device)) {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds + kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 } else {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds + kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 }
                 break;
             }
