@@ -123,6 +123,16 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
 #define PP_ST(p, v) (*(p) = (v))
 #define PP_LD(p) (*(p))
 #endif
+#ifndef PP_PATHS_NT            // emit_paths: every path point as a nontemporal (streaming) store
+#define PP_PATHS_NT 1
+#endif
+// one (x, y) path point: a 16-B store (p 16-B aligned: paths are [.., c] pairs of doubles)
+__device__ __forceinline__ void st_xy(double* p, double x, double y) {
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    const dv2 xy = {x, y};
+    if (PP_PATHS_NT) __builtin_nontemporal_store(xy, (dv2*)p);
+    else *(dv2*)p = xy;
+}
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
@@ -969,14 +979,33 @@ PP_PREP_GRP(k_prep_g16, 16)
 struct Slot {
     double *X, *Y, *A, *B, *C;
     int* meta;          // [0] n knots, [1] n control points, [2] first control-point knot, [3] flags
-    int64_t st;         // element stride
+    int64_t st;         // element stride of the knot arrays
+    int64_t mst;        // element stride of meta
     __device__ __forceinline__ double& x(int i) const { return X[i * st]; }
     __device__ __forceinline__ double& y(int i) const { return Y[i * st]; }
     __device__ __forceinline__ double& a(int i) const { return A[i * st]; }
     __device__ __forceinline__ double& b(int i) const { return B[i * st]; }
     __device__ __forceinline__ double& c(int i) const { return C[i * st]; }
-    __device__ __forceinline__ int& m(int k) const { return meta[k * st]; }
+    __device__ __forceinline__ int& m(int k) const { return meta[k * mst]; }
 };
+// k_cand's LDS slot j. PP_SLOT_AOS: knot-interleaved, knot i of slot j holds x, y, a, b, c at
+// sm[(j * kKP + i) * 5 + field] — one address register per slot and immediate offsets for the five
+// fields (the field-major layout needs five: in emit_paths mode they spill, and every reload waits
+// for the lane's outstanding path stores). Otherwise field-major, sX[j * kKP + i] etc.
+#ifndef PP_SLOT_AOS
+#define PP_SLOT_AOS 1
+#endif
+__device__ __forceinline__ Slot lds_slot(double* sX, int nslot, int* sMeta, int j) {
+#if PP_SLOT_AOS
+    (void)nslot;
+    double* b = sX + (int64_t)j * kKP * 5;
+    return Slot{b, b + 1, b + 2, b + 3, b + 4, sMeta + 4 * j, 5, 1};
+#else
+    const int64_t f = (int64_t)nslot * kKP;
+    double* b = sX + (int64_t)j * kKP;
+    return Slot{b, b + f, b + 2 * f, b + 3 * f, b + 4 * f, sMeta + 4 * j, 1, 1};
+#endif
+}
 constexpr int kMetaFallback = 1, kMetaTrunc = 2, kMetaWalkFail = 4;
 
 // s: scene (inputs, stride in.n_scenes); v: its prep record (stride Sv). The spline depends on the
@@ -1349,7 +1378,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 const double tx = pos_x * ca - pos_y * sa;
                 const double ty = pos_x * sa + pos_y * ca;
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) { px[ng * ps] = tx + cx; px[ng * ps + 1] = ty + cy; }
+                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, tx + cx, ty + cy);
             }
             if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
             ng++;
@@ -1649,7 +1678,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const double ty = pos_x * sa + pos_y * ca;
             if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
-                *(double2*)(px + ng * ps) = make_double2(tx + cx, ty + cy);     // one 16-B store (x, y)
+                st_xy(px + ng * ps, tx + cx, ty + cy);      // one 16-B store (x, y)
         }
         if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
         ng++;
@@ -1826,7 +1855,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         if (TS > 8) TS = 8;
         const int j = tid / TS, r = tid - j * TS;
         const bool act = j < NL * nsc && ((sSlow[j / NL] != 0) == kSlow);
-        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
+        const Slot sl = lds_slot(sX, nslot, sMeta, j);
         const int L = j % NL;
         const int64_t s = s0 + j / NL;
         LaneGeom g;
@@ -1838,7 +1867,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         // for them (a team layout spreads them over every wave of the block)
         const int js = tid;
         const bool act_s = js < NL * nsc && ((sSlow[js / NL] != 0) == kSlow);
-        const Slot sls = {sX + js * kKP, sY + js * kKP, sA + js * kKP, sB + js * kKP, sC + js * kKP, sMeta + 4 * js, 1};
+        const Slot sls = lds_slot(sX, nslot, sMeta, js);
         if (act_s) {
             const int64_t vs = (s0 + js / NL) * D;
             LaneGeom gs;
@@ -1867,7 +1896,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 #else
     if (tid < NL * nsc && ((sSlow[tid / NL] != 0) == kSlow)) {   // phase A
         const int j = tid;
-        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
+        const Slot sl = lds_slot(sX, nslot, sMeta, j);
         setup_lane(m, P, in, pv, s0 + j / NL, (s0 + j / NL) * D, Sv, j % NL, sl);
     }
 #endif
@@ -1903,7 +1932,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         const int64_t v = s * D + d;              // this draw's prep record
         const int L = cc / NS, k = cc - L * NS;
         const int j = sc_l * NL + L;
-        const Slot sl = {sX + j * kKP, sY + j * kKP, sA + j * kKP, sB + j * kKP, sC + j * kKP, sMeta + 4 * j, 1};
+        const Slot sl = lds_slot(sX, nslot, sMeta, j);
 #ifdef PP_CHECK
         {   // the slot was written by this group's phase A (not left over from an earlier group)
             const int nk_ = sl.m(0), ncp_ = sl.m(1), npk_ = sl.m(2);
@@ -1936,8 +1965,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             double* p0 = out.paths + ((s * N) * C + c) * 2;
             for (int i = 0; i < K; i++) {
                 if (!PP_CHKP(p0 + i * ps + 1, paths, npaths, 7)) break;
-                p0[i * ps] = in.prev_x[(int64_t)i * S + s];
-                p0[i * ps + 1] = in.prev_y[(int64_t)i * S + s];
+                st_xy(p0 + i * ps, in.prev_x[(int64_t)i * S + s], in.prev_y[(int64_t)i * S + s]);
             }
             double* px = p0 + K * ps;
             R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
@@ -1945,7 +1973,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                                                        px, ps);
             for (int i = R.ng; i < N - K; i++) {
                 if (!PP_CHKP(px + i * ps + 1, paths, npaths, 8)) break;
-                px[i * ps] = __builtin_nan(""); px[i * ps + 1] = __builtin_nan("");
+                st_xy(px + i * ps, __builtin_nan(""), __builtin_nan(""));
             }
             if (out.path_len && PP_CHK(s * C + c < g_lim.ncost, 11, s * C + c)) out.path_len[s * C + c] = K + R.ng;
             if (winner) {
@@ -2117,7 +2145,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     // slot arrays interleaved by lane ([knot][lane]) so the 64 lanes' accesses spread over banks
     const Slot sl = {wsm + j, wsm + kWinKnots * kWinBlock + j, wsm + 2 * kWinKnots * kWinBlock + j,
                      wsm + 3 * kWinKnots * kWinBlock + j, wsm + 4 * kWinKnots * kWinBlock + j,
-                     wmeta + j, kWinBlock};
+                     wmeta + j, kWinBlock, kWinBlock};
     setup_lane(m, P, in, pv, s, v0, Sv, L, sl);
     const double v = cand_speed(P, pv.ego_speed[v0], k);
     const SC sc = make_sc(P, pv, Sv, v0, L, v);
