@@ -130,6 +130,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="all-core leg threads (0: the host's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the extra weak-scaling measurement")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the host-buffer (PCIe-inclusive) side measurement")
+    ap.add_argument("--pcie-chunks", type=int, default=8,
+                    help="chunks of the host-buffer pipeline (H2D / evaluate / D2H overlapped across chunks)")
     ap.add_argument("--cpu-ranks", action="store_true",
                     help="launcher rehearsal without a GPU: every rank evaluates its shard with the CPU oracle")
     return ap.parse_args(argv)
@@ -220,6 +224,122 @@ def cpu_baseline(scenes_host_fn, S, prm, budget_s, threads):
             "value_1core": d1 * cand_per_scene / t1, "nproc": nproc, "cpu_model": model,
             "sample": f"{dn} scenes x {cand_per_scene} candidates of the same synthetic batch on {threads} "
                       f"threads ({tn:.1f} s), and {d1} scenes on 1 thread ({t1:.1f} s); {src}"}
+
+
+def chunk_bounds(S, chunks):
+    """Contiguous balanced scene ranges [lo, hi) of the host-buffer pipeline's chunks."""
+    k = max(1, min(chunks, S))
+    return [(i * S // k, (i + 1) * S // k) for i in range(k)]
+
+
+OUT_FIELDS = ("winner", "n_out", "next_x", "next_y", "cost", "status")
+
+
+def host_pipeline(m, scenes, prm, device, chunks, steps, warmup):
+    """PCIe-inclusive rate: the batch starts and ends in pinned host memory, as a
+    server handing pp_eval host buffers would see it. The batch is cut into `chunks` scene ranges;
+    chunk k's H2D copy, its pp_eval and its D2H copy (winner, n_out, next_x/y, costs, status) run
+    on three streams, double-buffered, so the copies of one chunk overlap the evaluation of the
+    next. Returns scenes/s-derived figures for the timed steps (the caller scales by candidates)."""
+    import torch
+    import ppamd
+    dev = torch.device("cuda", device)
+    S = int(scenes["ego_x"].shape[0])
+    bounds = chunk_bounds(S, chunks)
+    # pinned host copies of every chunk (chunk-shaped SoA, as a host caller would hold them)
+    h_sc = [{k: v[..., lo:hi].contiguous().cpu().pin_memory() for k, v in scenes.items()} for lo, hi in bounds]
+    h_res = [{k: v.pin_memory() for k, v in ppamd.alloc_result(hi - lo, prm, xp="torch", device="cpu").items()
+              if k in OUT_FIELDS} for lo, hi in bounds]
+    cmax = max(hi - lo for lo, hi in bounds)
+    # double buffers as flat storage sized for the largest chunk; chunk k uses compact views of
+    # its own shape over the front of them (the SoA layout [row * n + s] needs n as the stride)
+    d_sc = [{k: torch.empty(v[..., :1].numel() * cmax, dtype=v.dtype, device=dev) for k, v in scenes.items()}
+            for _ in range(2)]
+    r_tmpl = {k: v for k, v in ppamd.alloc_result(cmax, prm, xp="torch", device="cpu").items()}
+    d_res = [{k: torch.empty(v.numel(), dtype=v.dtype, device=dev) for k, v in r_tmpl.items()} for _ in range(2)]
+    s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
+    m.reserve(device, cmax)
+    h2d_bytes = sum(t.numel() * t.element_size() for c in h_sc for t in c.values())
+    d2h_bytes = sum(t.numel() * t.element_size() for c in h_res for t in c.values())
+
+    def compact(flat, shape):
+        n = 1
+        for x in shape:
+            n *= x
+        return flat[:n].view(shape)
+
+    def view(d, k):
+        return {f: compact(t, h_sc[k][f].shape) for f, t in d.items()}
+
+    def rview(d, k, n):
+        shapes = {f: (v.shape[0], n) if f in ("next_x", "next_y") else (n,) + tuple(v.shape[1:])
+                  for f, v in r_tmpl.items()}
+        return {f: compact(t, shapes[f]) for f, t in d.items()}
+
+    def one_step():
+        ev_cmp = [None] * len(bounds)
+        ev_d2h = [None] * len(bounds)
+        for k, (lo, hi) in enumerate(bounds):
+            n, b = hi - lo, k % 2
+            sc_k, rs_k = view(d_sc[b], k), rview(d_res[b], k, n)
+            with torch.cuda.stream(s_h2d):
+                if k >= 2:
+                    s_h2d.wait_event(ev_cmp[k - 2])          # chunk k-2 is done with d_sc[b]
+                for f, t in sc_k.items():
+                    t.copy_(h_sc[k][f], non_blocking=True)
+                e_in = torch.cuda.Event()
+                e_in.record(s_h2d)
+            s_cmp.wait_event(e_in)
+            if k >= 2:
+                s_cmp.wait_event(ev_d2h[k - 2])              # chunk k-2's results have left d_res[b]
+            ppamd.evaluate(m, sc_k, prm, rs_k, device=device, stream=s_cmp.cuda_stream)
+            ev_cmp[k] = torch.cuda.Event()
+            ev_cmp[k].record(s_cmp)
+            with torch.cuda.stream(s_d2h):
+                s_d2h.wait_event(ev_cmp[k])
+                for f in OUT_FIELDS:
+                    h_res[k][f].copy_(rs_k[f], non_blocking=True)
+                ev_d2h[k] = torch.cuda.Event()
+                ev_d2h[k].record(s_d2h)
+
+    for _ in range(warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+    # each step host buffer to host buffer, timed on its own (the copy engines' rate varies from step
+    # to step on the box): the median step is reported, the mean and the fastest beside it
+    per = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        one_step()
+        torch.cuda.synchronize(dev)
+        per.append(time.perf_counter() - t0)
+    el = float(np.median(per)) * steps
+
+    def copy_rate(h2d):
+        """One direction alone: every chunk's copies on one stream, GB/s."""
+        s = s_h2d if h2d else s_d2h
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        with torch.cuda.stream(s):
+            for k, (lo, hi) in enumerate(bounds):
+                if h2d:
+                    for f, d in view(d_sc[k % 2], k).items():
+                        d.copy_(h_sc[k][f], non_blocking=True)
+                else:
+                    for f, d in rview(d_res[k % 2], k, hi - lo).items():
+                        if f in OUT_FIELDS:
+                            h_res[k][f].copy_(d, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        return (h2d_bytes if h2d else d2h_bytes) / (time.perf_counter() - t) / 1e9
+
+    stats = {"scenes_per_s": S * steps / el, "ms_per_step": el / steps * 1e3, "chunks": len(bounds),
+             "ms_per_step_mean": float(np.mean(per)) * 1e3, "ms_per_step_min": float(np.min(per)) * 1e3,
+             "h2d_only_gb_per_s": copy_rate(True), "d2h_only_gb_per_s": copy_rate(False),
+             "h2d_bytes_per_step": h2d_bytes, "d2h_bytes_per_step": d2h_bytes,
+             "pcie_gb_per_s": (h2d_bytes + d2h_bytes) * steps / el / 1e9}
+    # the host-side outputs, reassembled in scene order (tests compare them with the resident path)
+    outs = {f: torch.cat([h[f] for h in h_res], dim=1 if f in ("next_x", "next_y") else 0) for f in OUT_FIELDS}
+    return stats, outs
 
 
 def run_cpu_ranks(a, rank, world, dist):
@@ -425,6 +545,19 @@ def main(argv=None):
                                           "tools/valu_peak.hip"}
     if a.rollout:
         out["scene_frames_per_s"] = total_scenes * a.steps * frames / elapsed
+    if world == 1 and not (a.no_pcie or a.rollout or a.emit_paths or D > 1):
+        # side measurement, never `value`: the same batch handed over in pinned host buffers
+        hp, _ = host_pipeline(m, scenes, prm, local, a.pcie_chunks, a.steps, min(a.warmup, 2))
+        out["pcie_inclusive"] = {"value": hp["scenes_per_s"] * Cn, "unit": "candidate trajectories/s",
+                                 "ms_per_step": hp["ms_per_step"], "ms_per_step_mean": hp["ms_per_step_mean"],
+                                 "ms_per_step_min": hp["ms_per_step_min"], "chunks": hp["chunks"],
+                                 "h2d_bytes_per_step": hp["h2d_bytes_per_step"],
+                                 "d2h_bytes_per_step": hp["d2h_bytes_per_step"],
+                                 "pcie_gb_per_s": hp["pcie_gb_per_s"],
+                                 "h2d_only_gb_per_s": hp["h2d_only_gb_per_s"],
+                                 "d2h_only_gb_per_s": hp["d2h_only_gb_per_s"],
+                                 "what": "scenes in pinned host memory, H2D + pp_eval + D2H of winner, n_out, "
+                                         "next_x/y, costs, status; chunks pipelined over 3 streams"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
         model, nproc, share = host_cpu()
         threads = a.cpu_threads or share
