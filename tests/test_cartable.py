@@ -17,21 +17,21 @@ import oracle_lib
 from oracle_lib import ppamd
 
 
-def many_car_scenes(m, S, seed, ids_fn):
-    """S synthetic scenes with 24 sensor_fusion rows: two generator batches' cars side by side,
-    rows reordered by the ids ids_fn(rng, 24) (ascending, as the batch contract requires)."""
-    a = ppamd.synth_host(m, S, seed=seed, first=0)
-    b = ppamd.synth_host(m, S, seed=seed + 1, first=0)
-    sc = {k: v for k, v in a.items()}
+def many_car_scenes(m, S, seed, ids_fn, rows=24):
+    """S synthetic scenes with `rows` sensor_fusion rows: the cars of ceil(rows / 12) generator
+    batches side by side, rows reordered by the ids ids_fn(rng, rows) (ascending, as the batch
+    contract requires); every 7th scene reports 5 rows fewer."""
+    bs = [ppamd.synth_host(m, S, seed=seed + i, first=0) for i in range((rows + 11) // 12)]
+    sc = {k: v for k, v in bs[0].items()}
     for k in ("car_x", "car_y", "car_vx", "car_vy"):
-        sc[k] = np.ascontiguousarray(np.concatenate([a[k], b[k]], 0))
+        sc[k] = np.ascontiguousarray(np.concatenate([b[k] for b in bs], 0)[:rows])
     rng = np.random.default_rng(seed)
-    ids = np.zeros((24, S), np.int32)
+    ids = np.zeros((rows, S), np.int32)
     for s in range(S):
-        ids[:, s] = np.sort(ids_fn(rng, 24))
+        ids[:, s] = np.sort(ids_fn(rng, rows))
     sc["car_id"] = ids
-    sc["n_cars"] = np.full(S, 24, np.int32)
-    sc["n_cars"][::7] = 19
+    sc["n_cars"] = np.full(S, rows, np.int32)
+    sc["n_cars"][::7] = rows - 5
     return sc
 
 
@@ -44,12 +44,13 @@ def ids_wide(rng, n):
     return rng.choice(np.unique(pool), n, replace=False)
 
 
-def test_restatement_equals_reference_many_cars():
+@pytest.mark.parametrize("rows", [24, ppamd.MAX_CARS])
+def test_restatement_equals_reference_many_cars(rows):
     rlib = oracle_lib.load_ref()
     olib = oracle_lib.load_oracle()
     wx, wy = oracle_lib.highway_map()
     m = ppamd.Map(wx, wy)
-    sc = many_car_scenes(m, 600, 4711, ids_wide)
+    sc = many_car_scenes(m, 600 if rows <= 24 else 200, 4711, ids_wide, rows)
     prm = ppamd.default_params(n_speeds=5)
     ref = oracle_lib.ref_eval(rlib, wx, wy, sc, 5, [prm.speed_offsets[i] for i in range(4)])
     got = oracle_lib.oracle_eval(olib, wx, wy, sc, ppamd.default_params(n_speeds=5, emit_paths=True), info=True)
@@ -168,17 +169,28 @@ class TestCarTableGPU:
         return {"torch": torch, "m": ppamd.Map(wx, wy), "wx": wx, "wy": wy, "dev": torch.device("cuda", 0),
                 "olib": oracle_lib.load_oracle(), "rlib": oracle_lib.load_ref_session()}
 
-    def test_eval_many_cars_vs_oracle(self, env):
-        sc = many_car_scenes(env["m"], 1500, 99, ids_wide)
+    @pytest.mark.parametrize("rows", [24, ppamd.MAX_CARS])
+    def test_eval_many_cars_vs_oracle(self, env, rows):
+        S = 1500 if rows <= 24 else 600
+        sc = many_car_scenes(env["m"], S, 99, ids_wide, rows)
         for mode in (ppamd.COST_REFERENCE, ppamd.COST_COMFORT):
             prm = ppamd.default_params(emit_paths=True, cost_mode=mode)
             d = {k: env["torch"].from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
-            r = ppamd.alloc_result(1500, prm, xp="torch", device=env["dev"])
+            r = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
             ppamd.evaluate(env["m"], d, prm, r, device=0)
             env["torch"].cuda.synchronize()
             got = ppamd.result_to_numpy(r)
             ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
             oracle_lib.compare(got, ref)
+
+    def test_eval_rejects_more_rows_than_max(self, env):
+        """car_stride > PP_MAX_CARS: PP_ERR_ARG before any launch (include/pp.h), never a truncation"""
+        sc = many_car_scenes(env["m"], 64, 5, ids_wide, ppamd.MAX_CARS + 1)
+        prm = ppamd.default_params()
+        d = {k: env["torch"].from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
+        r = ppamd.alloc_result(64, prm, xp="torch", device=env["dev"])
+        with pytest.raises(ppamd.PPError):
+            ppamd.evaluate(env["m"], d, prm, r, device=0)
 
     @pytest.mark.parametrize("ids,sensor_range,seed,need", [
         (list(range(1000, 1000 + 7 * 24, 7)), 60.0, 3, "stale"),   # 24 cars, ids >= 16, stale entries
