@@ -314,6 +314,9 @@ def host_pipeline(m, scenes, prm, device, chunks, steps, warmup):
         torch.cuda.synchronize(dev)
         per.append(time.perf_counter() - t0)
     el = float(np.median(per)) * steps
+    # the host-side outputs, reassembled in scene order before copy_rate below reuses the buffers
+    # (tests compare them with the resident path)
+    outs = {f: torch.cat([h[f] for h in h_res], dim=1 if f in ("next_x", "next_y") else 0) for f in OUT_FIELDS}
 
     def copy_rate(h2d):
         """One direction alone: every chunk's copies on one stream, GB/s."""
@@ -337,8 +340,6 @@ def host_pipeline(m, scenes, prm, device, chunks, steps, warmup):
              "h2d_only_gb_per_s": copy_rate(True), "d2h_only_gb_per_s": copy_rate(False),
              "h2d_bytes_per_step": h2d_bytes, "d2h_bytes_per_step": d2h_bytes,
              "pcie_gb_per_s": (h2d_bytes + d2h_bytes) * steps / el / 1e9}
-    # the host-side outputs, reassembled in scene order (tests compare them with the resident path)
-    outs = {f: torch.cat([h[f] for h in h_res], dim=1 if f in ("next_x", "next_y") else 0) for f in OUT_FIELDS}
     return stats, outs
 
 

@@ -136,6 +136,46 @@ __device__ __forceinline__ void st_xy(double* p, double x, double y) {
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
+// Winner record layout (k_cand -> k_emit). 0 (product): two point-major arrays, pos_x at
+// rec[g S + s], pos_y at rec[room S + g S + s], the rotation of an adjusted step at
+// rec[2 room S + g S + s]. PP_REC_PAIR 1 (measured slower, profiles/r02_ablations.txt): step g of
+// scene s keeps its local position as one 16-B (pos_x, pos_y) pair at rec[2 (g S + s)], the
+// rotations behind the pairs of the longest walk, rec[2 N S + g S + s].
+#ifndef PP_REC_PAIR
+#define PP_REC_PAIR 0
+#endif
+typedef double pp_dv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void rec_st(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
+                                       double x, double y) {
+    if (PP_REC_PAIR) {
+        const pp_dv2 xy = {x, y};
+        pp_dv2* p = (pp_dv2*)(rec + 2 * (g * S + s));
+        if (PP_NT) __builtin_nontemporal_store(xy, p); else *p = xy;
+    } else {
+        PP_ST(rec + g * S + s, x);
+        PP_ST(rec + rstride + g * S + s, y);
+    }
+}
+__device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
+                                       double& x, double& y) {
+    if (PP_REC_PAIR) {
+        const pp_dv2* p = (const pp_dv2*)(rec + 2 * (g * S + s));
+        const pp_dv2 xy = PP_NT ? __builtin_nontemporal_load(p) : *p;
+        x = xy.x; y = xy.y;
+    } else {
+        x = PP_LD(rec + g * S + s);
+        y = PP_LD(rec + rstride + g * S + s);
+    }
+}
+// offset of the rotation entries: behind the pairs of the longest walk (2 N S: the pairs of scenes
+// with different room interleave, so the rotations cannot start at a per-scene 2 room S), or
+// behind the two per-scene arrays (2 room S; every address of scene s is = s mod S there)
+__device__ __forceinline__ int64_t rec_rot_off(int64_t rstride, int N, int64_t S) {
+    return PP_REC_PAIR ? 2 * (int64_t)N * S : 2 * rstride;
+}
+// the bound-check addresses of step g's pair (PP_CHECK builds)
+#define PP_REC_X(rec, rstride, g, S, s) (PP_REC_PAIR ? (rec) + 2 * ((g) * (S) + (s)) : (rec) + (g) * (S) + (s))
+#define PP_REC_Y(rec, rstride, g, S, s) (PP_REC_PAIR ? (rec) + 2 * ((g) * (S) + (s)) + 1 : (rec) + (rstride) + (g) * (S) + (s))
 #ifndef PP_EMIT_ROTATE
 #define PP_EMIT_ROTATE 1
 #endif
@@ -1334,8 +1374,9 @@ template <bool kLarge, int kOutMode, bool kCache>
 __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
                                  double angle, double ca0, double sa0, SC sc, int room, double* wx,
                                  double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true,
-                                 double* rec = nullptr, int dcls = 0) {
+                                 double* rec = nullptr, int dcls = 0, int64_t rs = 0) {
     (void)dcls;   // PP_DIAG builds: candidate class (|L - ego lane|) for the census
+    // kOutMode 3: rec = the record base + rs (the scene), ws = the batch's scene count (rec_st)
     const bool kOut = kOutMode == 2 || (kOutMode == 1 && out_on);
     const bool kRec = kOutMode == 3 && out_on;
     const int64_t rstride = (int64_t)room * ws;
@@ -1380,7 +1421,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
                 if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, tx + cx, ty + cy);
             }
-            if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
+            if (kOutMode == 3 && kRec && PP_CHKP(PP_REC_X(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(PP_REC_Y(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
             ng++;
             R.travelled += dstep;
         }
@@ -1635,8 +1676,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     double nad = kLarge ? nc / speed / 50
                                         : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
-                    if (PP_CHKP(rec + 2 * rstride + ng * ws, rec, nrec, 6))
-                        PP_ST(rec + 2 * rstride + ng * ws, nad - adiff);   // rot (src/main.cpp:986)
+                    const int64_t roff = rec_rot_off(rstride, P.n_points, ws);
+                    if (PP_CHKP(rec + roff + ng * ws, rec, nrec, 6))
+                        PP_ST(rec + roff + ng * ws, nad - adiff);   // rot (src/main.cpp:986)
                     const uint64_t bit = 1ull << (ng & 63);
                     if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
                 }
@@ -1680,7 +1722,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 st_xy(px + ng * ps, tx + cx, ty + cy);      // one 16-B store (x, y)
         }
-        if (kOutMode == 3 && kRec && PP_CHKP(rec + ng * ws, rec, nrec, 4) && PP_CHKP(rec + rstride + ng * ws, rec, nrec, 5)) { PP_ST(rec + ng * ws, pos_x); PP_ST(rec + rstride + ng * ws, pos_y); }
+        if (kOutMode == 3 && kRec && PP_CHKP(PP_REC_X(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(PP_REC_Y(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -1757,10 +1799,10 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
         for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 19); }
+            if (g < ng) { PP_CHKP(PP_REC_Y(rec, rstride, (int64_t)g, S, s), rec, nrec, 19); }
 #endif
-            px_[u] = g < ng ? PP_LD(rec + (int64_t)g * S + s) : 0.0;
-            py_[u] = g < ng ? PP_LD(rec + rstride + (int64_t)g * S + s) : 0.0;
+            px_[u] = 0.0; py_[u] = 0.0;
+            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
         }
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
@@ -2019,7 +2061,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             // reference mode, the block's first wave: the winners record their local path
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
             R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
-                                                       S, nullptr, 0, winner, rec + s);
+                                                       S, nullptr, 0, winner, rec + s, 0, s);
             if (winner && emit_in) {          // in-block K4 below: step count and masks in LDS
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
@@ -2061,7 +2103,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             const uint64_t mm = gs < 64 ? sAdj[2 * w] : sAdj[2 * w + 1];
             if (!((mm >> (gs & 63)) & 1)) continue;
             const int64_t s = s0 + w;
-            const double* rr = rec + 2 * (int64_t)(N - pv.K[s]) * S + (int64_t)gs * S + s;
+            const double* rr = rec + rec_rot_off((int64_t)(N - pv.K[s]) * S, N, S) + (int64_t)gs * S + s;
             if (!PP_CHKP(rr, rec, nrec, 18)) continue;
             const double rt = *rr;
             double sr, cr;
@@ -2182,6 +2224,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     const int room = N - K;
     const int ng = out.n_out[s] - K;
     const int64_t rstride = (int64_t)room * S;
+    const int64_t roff = rec_rot_off(rstride, N, S);
     {   // the kept previous points: every load issued before the first store
         double kx[PP_PREV_KEEP], ky[PP_PREV_KEEP];
 #pragma unroll
@@ -2226,12 +2269,12 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
             bits |= bit ? 1u << u : 0u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(rec + rstride + (int64_t)g * S + s, rec, nrec, 16); }
-            if (bit) { PP_CHKP(rec + 2 * rstride + (int64_t)g * S + s, rec, nrec, 16); }
+            if (g < ng) { PP_CHKP(PP_REC_Y(rec, rstride, (int64_t)g, S, s), rec, nrec, 16); }
+            if (bit) { PP_CHKP(rec + roff + (int64_t)g * S + s, rec, nrec, 16); }
 #endif
-            px_[u] = g < ng ? PP_LD(rec + (int64_t)g * S + s) : 0.0;
-            py_[u] = g < ng ? PP_LD(rec + rstride + (int64_t)g * S + s) : 0.0;
-            rt[u] = bit ? PP_LD(rec + 2 * rstride + (int64_t)g * S + s) : 0.0;
+            px_[u] = 0.0; py_[u] = 0.0;
+            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
+            rt[u] = bit ? PP_LD(rec + roff + (int64_t)g * S + s) : 0.0;
         }
         bool huge = false;
 #pragma unroll
@@ -2239,12 +2282,13 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         if (__builtin_expect(huge, 0)) {
             for (int g = g0; g < ng && g < g0 + kEmitChunk; g++) {
                 if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
-                    const double rot = rec[2 * rstride + (int64_t)g * S + s];
+                    const double rot = rec[roff + (int64_t)g * S + s];
                     double cr, sr;
                     ppm::sincos_pp<true>(rot, sr, cr);
                     rotate(rot, cr, sr);
                 }
-                const double qx = rec[(int64_t)g * S + s], qy = rec[rstride + (int64_t)g * S + s];
+                double qx, qy;
+                rec_ld(rec, rstride, g, S, s, qx, qy);
                 out.next_x[(int64_t)(K + g) * S + s] = (qx * ca - qy * sa) + cx;
                 out.next_y[(int64_t)(K + g) * S + s] = (qx * sa + qy * ca) + cy;
                 pxp = qx;
@@ -2255,9 +2299,17 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         // sin/cos of the chunk's turns first (rt = 0 where no turn): independent of each other and
         // of the chain of turns below, so they overlap instead of queueing behind it
         double crs[kEmitChunk], srs[kEmitChunk];
+#ifdef PP_ABL_EMIT_NOROT    // diagnostic timing build (wrong results): no turn is replayed
+        bits = 0;
+#endif
         if (bits) {
+#ifdef PP_ABL_EMIT_TRIG     // diagnostic timing build (wrong results): first-order sin/cos of the turns
+#pragma unroll
+            for (int u = 0; u < kEmitChunk; u++) { srs[u] = rt[u]; crs[u] = 1.0; }
+#else
 #pragma unroll
             for (int u = 0; u < kEmitChunk; u++) ppm::sincos_pp<false>(rt[u], srs[u], crs[u]);
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kEmitChunk; u++) {
@@ -2278,7 +2330,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     for (int g = 0; g < ng; g++) {
         const uint64_t bit = g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1;
         if (bit) {
-            const double rot = rec[2 * rstride + (int64_t)g * S + s];
+            const double rot = rec[roff + (int64_t)g * S + s];
             double tpx = pxp * ca - pyp * sa;
             double tpy = pxp * sa + pyp * ca;
             tpx = tpx + cx;
@@ -2293,7 +2345,8 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             tangle += rot;
             ppm::sincos_pp<true>(tangle, sa, ca);
         }
-        const double px_ = rec[(int64_t)g * S + s], py_ = rec[rstride + (int64_t)g * S + s];
+        double px_, py_;
+        rec_ld(rec, rstride, g, S, s, px_, py_);
         const double tx = px_ * ca - py_ * sa;
         const double ty = px_ * sa + py_ * ca;
         out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
