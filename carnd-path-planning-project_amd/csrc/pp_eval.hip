@@ -136,46 +136,57 @@ __device__ __forceinline__ void st_xy(double* p, double x, double y) {
 #ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
 #define PP_EMIT_CHUNK 4
 #endif
-// Winner record layout (k_cand -> k_emit). 0 (product): two point-major arrays, pos_x at
-// rec[g S + s], pos_y at rec[room S + g S + s], the rotation of an adjusted step at
-// rec[2 room S + g S + s]. PP_REC_PAIR 1 (measured slower, profiles/r02_ablations.txt): step g of
-// scene s keeps its local position as one 16-B (pos_x, pos_y) pair at rec[2 (g S + s)], the
-// rotations behind the pairs of the longest walk, rec[2 N S + g S + s].
+// Winner record layout (k_cand -> k_emit); room = N - K steps of scene s, rstride = room S.
+//   0 (product): point-major arrays, pos_x at rec[g S + s], pos_y at rec[rstride + g S + s], the
+//     rotation of an adjusted step at rec[2 rstride + g S + s] (every address of scene s is = s mod S);
+//   1 (PP_REC_PAIR=1, measured slower): one 16-B (pos_x, pos_y) pair at rec[2 (g S + s)], the
+//     rotations behind the pairs of the longest walk, rec[2 N S + g S + s];
+//   2 (PP_REC_PAIR=2): wave-blocked, the 64 scenes of a wave own one contiguous 3 N x 64 block:
+//     pos_x at rec[B + g 64 + l], pos_y at rec[B + (N + g) 64 + l], rotation at rec[B + (2N + g) 64
+//     + l], B = (s / 64) 3 N 64, l = s mod 64 (a wave's record is 3 N 512 contiguous bytes instead
+//     of 3 N rows S 8 bytes apart; the buffer's scene capacity is a multiple of 64).
 #ifndef PP_REC_PAIR
 #define PP_REC_PAIR 0
 #endif
 typedef double pp_dv2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void rec_st(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
+__device__ __forceinline__ int64_t rec_wb(int N, int64_t s) { return (s >> 6) * (3 * (int64_t)N * 64) + (s & 63); }
+__device__ __forceinline__ double* rec_px(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
+    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + g * 64 : PP_REC_PAIR == 1 ? rec + 2 * (g * S + s) : rec + g * S + s;
+}
+__device__ __forceinline__ double* rec_py(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
+    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + ((int64_t)N + g) * 64
+         : PP_REC_PAIR == 1 ? rec + 2 * (g * S + s) + 1 : rec + rstride + g * S + s;
+}
+__device__ __forceinline__ double* rec_rot(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
+    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + (2 * (int64_t)N + g) * 64
+         : PP_REC_PAIR == 1 ? rec + 2 * (int64_t)N * S + g * S + s : rec + 2 * rstride + g * S + s;
+}
+__device__ __forceinline__ const double* rec_rot(const double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
+    return rec_rot((double*)rec, rstride, N, g, S, s);
+}
+__device__ __forceinline__ void rec_st(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s,
                                        double x, double y) {
-    if (PP_REC_PAIR) {
+    if (PP_REC_PAIR == 1) {
         const pp_dv2 xy = {x, y};
-        pp_dv2* p = (pp_dv2*)(rec + 2 * (g * S + s));
+        pp_dv2* p = (pp_dv2*)rec_px(rec, rstride, N, g, S, s);
         if (PP_NT) __builtin_nontemporal_store(xy, p); else *p = xy;
     } else {
-        PP_ST(rec + g * S + s, x);
-        PP_ST(rec + rstride + g * S + s, y);
+        PP_ST(rec_px(rec, rstride, N, g, S, s), x);
+        PP_ST(rec_py(rec, rstride, N, g, S, s), y);
     }
 }
-__device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
+__device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s,
                                        double& x, double& y) {
-    if (PP_REC_PAIR) {
-        const pp_dv2* p = (const pp_dv2*)(rec + 2 * (g * S + s));
+    double* r = (double*)rec;
+    if (PP_REC_PAIR == 1) {
+        const pp_dv2* p = (const pp_dv2*)rec_px(r, rstride, N, g, S, s);
         const pp_dv2 xy = PP_NT ? __builtin_nontemporal_load(p) : *p;
         x = xy.x; y = xy.y;
     } else {
-        x = PP_LD(rec + g * S + s);
-        y = PP_LD(rec + rstride + g * S + s);
+        x = PP_LD(rec_px(r, rstride, N, g, S, s));
+        y = PP_LD(rec_py(r, rstride, N, g, S, s));
     }
 }
-// offset of the rotation entries: behind the pairs of the longest walk (2 N S: the pairs of scenes
-// with different room interleave, so the rotations cannot start at a per-scene 2 room S), or
-// behind the two per-scene arrays (2 room S; every address of scene s is = s mod S there)
-__device__ __forceinline__ int64_t rec_rot_off(int64_t rstride, int N, int64_t S) {
-    return PP_REC_PAIR ? 2 * (int64_t)N * S : 2 * rstride;
-}
-// the bound-check addresses of step g's pair (PP_CHECK builds)
-#define PP_REC_X(rec, rstride, g, S, s) (PP_REC_PAIR ? (rec) + 2 * ((g) * (S) + (s)) : (rec) + (g) * (S) + (s))
-#define PP_REC_Y(rec, rstride, g, S, s) (PP_REC_PAIR ? (rec) + 2 * ((g) * (S) + (s)) + 1 : (rec) + (rstride) + (g) * (S) + (s))
 #ifndef PP_EMIT_ROTATE
 #define PP_EMIT_ROTATE 1
 #endif
@@ -1421,7 +1432,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
                 if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, tx + cx, ty + cy);
             }
-            if (kOutMode == 3 && kRec && PP_CHKP(PP_REC_X(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(PP_REC_Y(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
+            if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, P.n_points, ng, ws, rs, pos_x, pos_y);
             ng++;
             R.travelled += dstep;
         }
@@ -1676,9 +1687,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     double nad = kLarge ? nc / speed / 50
                                         : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
-                    const int64_t roff = rec_rot_off(rstride, P.n_points, ws);
-                    if (PP_CHKP(rec + roff + ng * ws, rec, nrec, 6))
-                        PP_ST(rec + roff + ng * ws, nad - adiff);   // rot (src/main.cpp:986)
+                    double* rp = rec_rot(rec - rs, rstride, P.n_points, ng, ws, rs);
+                    if (PP_CHKP(rp, rec, nrec, 6))
+                        PP_ST(rp, nad - adiff);   // rot (src/main.cpp:986)
                     const uint64_t bit = 1ull << (ng & 63);
                     if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
                 }
@@ -1722,7 +1733,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 st_xy(px + ng * ps, tx + cx, ty + cy);      // one 16-B store (x, y)
         }
-        if (kOutMode == 3 && kRec && PP_CHKP(PP_REC_X(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(PP_REC_Y(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
+        if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, P.n_points, ng, ws, rs, pos_x, pos_y);
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -1799,10 +1810,10 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
         for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(PP_REC_Y(rec, rstride, (int64_t)g, S, s), rec, nrec, 19); }
+            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, N, g, S, s), rec, nrec, 19); }
 #endif
             px_[u] = 0.0; py_[u] = 0.0;
-            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
+            if (g < ng) rec_ld(rec, rstride, N, g, S, s, px_[u], py_[u]);
         }
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
@@ -2103,7 +2114,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             const uint64_t mm = gs < 64 ? sAdj[2 * w] : sAdj[2 * w + 1];
             if (!((mm >> (gs & 63)) & 1)) continue;
             const int64_t s = s0 + w;
-            const double* rr = rec + rec_rot_off((int64_t)(N - pv.K[s]) * S, N, S) + (int64_t)gs * S + s;
+            const double* rr = rec_rot(rec, (int64_t)(N - pv.K[s]) * S, N, gs, S, s);
             if (!PP_CHKP(rr, rec, nrec, 18)) continue;
             const double rt = *rr;
             double sr, cr;
@@ -2224,7 +2235,6 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     const int room = N - K;
     const int ng = out.n_out[s] - K;
     const int64_t rstride = (int64_t)room * S;
-    const int64_t roff = rec_rot_off(rstride, N, S);
     {   // the kept previous points: every load issued before the first store
         double kx[PP_PREV_KEEP], ky[PP_PREV_KEEP];
 #pragma unroll
@@ -2269,12 +2279,12 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
             bits |= bit ? 1u << u : 0u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(PP_REC_Y(rec, rstride, (int64_t)g, S, s), rec, nrec, 16); }
-            if (bit) { PP_CHKP(rec + roff + (int64_t)g * S + s, rec, nrec, 16); }
+            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, N, g, S, s), rec, nrec, 16); }
+            if (bit) { PP_CHKP(rec_rot(rec, rstride, N, g, S, s), rec, nrec, 16); }
 #endif
             px_[u] = 0.0; py_[u] = 0.0;
-            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
-            rt[u] = bit ? PP_LD(rec + roff + (int64_t)g * S + s) : 0.0;
+            if (g < ng) rec_ld(rec, rstride, N, g, S, s, px_[u], py_[u]);
+            rt[u] = bit ? PP_LD(rec_rot(rec, rstride, N, g, S, s)) : 0.0;
         }
         bool huge = false;
 #pragma unroll
@@ -2282,13 +2292,13 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         if (__builtin_expect(huge, 0)) {
             for (int g = g0; g < ng && g < g0 + kEmitChunk; g++) {
                 if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
-                    const double rot = rec[roff + (int64_t)g * S + s];
+                    const double rot = *rec_rot(rec, rstride, N, g, S, s);
                     double cr, sr;
                     ppm::sincos_pp<true>(rot, sr, cr);
                     rotate(rot, cr, sr);
                 }
                 double qx, qy;
-                rec_ld(rec, rstride, g, S, s, qx, qy);
+                rec_ld(rec, rstride, N, g, S, s, qx, qy);
                 out.next_x[(int64_t)(K + g) * S + s] = (qx * ca - qy * sa) + cx;
                 out.next_y[(int64_t)(K + g) * S + s] = (qx * sa + qy * ca) + cy;
                 pxp = qx;
@@ -2330,7 +2340,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     for (int g = 0; g < ng; g++) {
         const uint64_t bit = g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1;
         if (bit) {
-            const double rot = rec[roff + (int64_t)g * S + s];
+            const double rot = *rec_rot(rec, rstride, N, g, S, s);
             double tpx = pxp * ca - pyp * sa;
             double tpy = pxp * sa + pyp * ca;
             tpx = tpx + cx;
@@ -2346,7 +2356,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             ppm::sincos_pp<true>(tangle, sa, ca);
         }
         double px_, py_;
-        rec_ld(rec, rstride, g, S, s, px_, py_);
+        rec_ld(rec, rstride, N, g, S, s, px_, py_);
         const double tx = px_ * ca - py_ * sa;
         const double ty = px_ * sa + py_ * ca;
         out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
@@ -2913,10 +2923,11 @@ int ensure_ws(StreamWS& W, hipStream_t st, int64_t Sv) {
 }
 
 int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
-    if (W.rec_cap >= S) return PP_OK;
+    const int64_t cap = (S + 63) & ~(int64_t)63;   // whole 64-scene blocks (PP_REC_PAIR 2)
+    if (W.rec_cap >= cap) return PP_OK;
     if (W.rec) { (void)hipStreamSynchronize(st); (void)hipFree(W.rec); W.rec = nullptr; W.rec_cap = 0; }
-    if (hipMalloc(&W.rec, rec_bytes(S)) != hipSuccess) return PP_ERR_NOMEM;
-    W.rec_cap = S;
+    if (hipMalloc(&W.rec, rec_bytes(cap)) != hipSuccess) return PP_ERR_NOMEM;
+    W.rec_cap = cap;
     return PP_OK;
 }
 
