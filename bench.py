@@ -402,6 +402,10 @@ def main(argv=None):
 
     import torch
     import ppamd
+    # one GPU per local rank; more local ranks than GPUs share them round-robin (a rehearsal of the
+    # N-rank path on a smaller box: a per-GPU timing is then not a scaling figure)
+    ngpu = torch.cuda.device_count()
+    local = local % ngpu if ngpu else local
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     wx, wy = ppamd.highway_map()
@@ -474,6 +478,32 @@ def main(argv=None):
     if dist:
         per_rank = [None] * world
         dist.all_gather_object(per_rank, kms)
+    pcie = None
+    if not (a.no_pcie or a.rollout or a.emit_paths or D > 1):
+        # side measurement, never `value`: the same batch handed over in pinned host buffers, every
+        # rank its own shard through its own link; the job's step is the slowest rank's median step
+        if dist:
+            dist.barrier()
+        try:
+            hp, _ = host_pipeline(m, scenes, prm, local, a.pcie_chunks, a.steps, min(a.warmup, 2))
+            err = None
+        except Exception as ex:         # a side measurement never takes the bench line down
+            hp, err = None, f"{type(ex).__name__}: {ex}"
+        # every rank reaches the MAX (a failed rank reports inf), so no rank waits for a lost peer
+        ms_max = max_over_ranks(hp["ms_per_step"] if hp else float("inf"), dist)
+        if hp is None or ms_max == float("inf"):
+            pcie = {"error": err or "failed on another rank"}
+        else:
+            pcie = {"value": total_scenes * Cn / (ms_max * 1e-3), "unit": "candidate trajectories/s",
+                    "ms_per_step": ms_max, "ms_per_step_mean": hp["ms_per_step_mean"],
+                    "ms_per_step_min": hp["ms_per_step_min"], "chunks": hp["chunks"],
+                    "h2d_bytes_per_step": hp["h2d_bytes_per_step"] * world,
+                    "d2h_bytes_per_step": hp["d2h_bytes_per_step"] * world,
+                    "pcie_gb_per_s_per_gpu": hp["pcie_gb_per_s"],
+                    "h2d_only_gb_per_s": hp["h2d_only_gb_per_s"],
+                    "d2h_only_gb_per_s": hp["d2h_only_gb_per_s"],
+                    "what": "scenes in pinned host memory, H2D + pp_eval + D2H of winner, n_out, next_x/y, "
+                            "costs, status; chunks pipelined over 3 streams; per-rank figures are rank 0's"}
     weak = None
     if world > 1 and not a.no_weak and a.scaling == "strong":
         del scenes
@@ -525,6 +555,8 @@ def main(argv=None):
     }
     if weak:
         out["weak_scaling"] = weak
+    if pcie:
+        out["pcie_inclusive"] = pcie
     # the bound that matters for this path: FP64 VALU issue (no MFMA-shaped work, HBM a few %)
     peak, peak_add = load_valu_peak()
     if pmc and peak:
@@ -546,19 +578,6 @@ def main(argv=None):
                                           "tools/valu_peak.hip"}
     if a.rollout:
         out["scene_frames_per_s"] = total_scenes * a.steps * frames / elapsed
-    if world == 1 and not (a.no_pcie or a.rollout or a.emit_paths or D > 1):
-        # side measurement, never `value`: the same batch handed over in pinned host buffers
-        hp, _ = host_pipeline(m, scenes, prm, local, a.pcie_chunks, a.steps, min(a.warmup, 2))
-        out["pcie_inclusive"] = {"value": hp["scenes_per_s"] * Cn, "unit": "candidate trajectories/s",
-                                 "ms_per_step": hp["ms_per_step"], "ms_per_step_mean": hp["ms_per_step_mean"],
-                                 "ms_per_step_min": hp["ms_per_step_min"], "chunks": hp["chunks"],
-                                 "h2d_bytes_per_step": hp["h2d_bytes_per_step"],
-                                 "d2h_bytes_per_step": hp["d2h_bytes_per_step"],
-                                 "pcie_gb_per_s": hp["pcie_gb_per_s"],
-                                 "h2d_only_gb_per_s": hp["h2d_only_gb_per_s"],
-                                 "d2h_only_gb_per_s": hp["d2h_only_gb_per_s"],
-                                 "what": "scenes in pinned host memory, H2D + pp_eval + D2H of winner, n_out, "
-                                         "next_x/y, costs, status; chunks pipelined over 3 streams"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
         model, nproc, share = host_cpu()
         threads = a.cpu_threads or share

@@ -2868,9 +2868,17 @@ constexpr int kMaxChunks = 16;
 #ifndef PP_PIPE_CHUNKS
 #define PP_PIPE_CHUNKS 1
 #endif
+// PP_SPLIT=n (experiment): n chunks, each a whole K1 -> K2 -> K4 pipeline of its own, chunks
+// alternating between the caller's stream and the auxiliary one (no event between the streams
+// until the join), instead of the K2-on-one-stream pipeline above
+int pipe_split() {
+    const char* e = getenv("PP_SPLIT");
+    return e && *e ? atoi(e) : 0;
+}
 int pipe_chunks(int64_t S, int64_t groups) {
     const char* e = getenv("PP_CHUNKS");
-    int n = e && *e ? atoi(e) : (S >= kPipeMin ? PP_PIPE_CHUNKS : 1);
+    const int sp = pipe_split();
+    int n = sp > 1 ? sp : e && *e ? atoi(e) : (S >= kPipeMin ? PP_PIPE_CHUNKS : 1);
     if (n > kMaxChunks) n = kMaxChunks;
     while (n > 1 && groups < 64LL * n) n--;
     return n < 1 ? 1 : n;
@@ -3302,7 +3310,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         auto g_lo = [&](int c) { return std::min<int64_t>((int64_t)c * gstep, cg.groups); };
         auto s_lo = [&](int c) { return std::min<int64_t>(g_lo(c) * cg.spb, S); };
         prep_lds_attr();
-        auto prep = [&](int c) {
+        auto prep = [&](int c, hipStream_t ax) {
             GroupBits gc = gb;
             gc.count = gb.count + c;
             gc.list = gb.list + g_lo(c);
@@ -3317,7 +3325,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 else hipLaunchKernelGGL((k_prep<false, false>), dim3(blocks), dim3(256), kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
             }
         };
-        auto emit = [&](int c) {
+        auto emit = [&](int c, hipStream_t ax) {
             const int64_t s0 = s_lo(c), s1 = s_lo(c + 1);
             if (s1 <= s0) return;
             hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)((s1 - s0 + 255) / 256)), dim3(256), 0, ax, B, P,
@@ -3326,7 +3334,33 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t) * nch, st) != hipSuccess) return PP_ERR_HIP;
         if (timing) (void)hipEventRecord(ev[0], st);
         if (hipEventRecord(e_start, st) != hipSuccess || hipStreamWaitEvent(ax, e_start, 0) != hipSuccess) return PP_ERR_HIP;
-        for (int c = 0; c < 2 && c < nch; c++) { prep(c); if (hipEventRecord(pe[c], ax) != hipSuccess) return PP_ERR_HIP; }
+        if (pipe_split() > 1) {      // whole pipelines per chunk, alternating streams (timing: all in "k_cand")
+            if (timing) (void)hipEventRecord(ev[1], st);
+            const char* stg = getenv("PP_SPLIT_STAGGER");
+            const int stagger = stg && *stg ? atoi(stg) : 0;
+            for (int c = 0; c < nch; c++) {
+                hipStream_t sc = (c & 1) ? ax : st;
+                // stagger 1: chunk c starts after chunk c - 1's K1 (its K2 then runs beside the other
+                // stream's K2 tail and K4); 2: after chunk c - 1's K2
+                if (stagger && c > 0 && hipStreamWaitEvent(sc, pe[c - 1], 0) != hipSuccess) return PP_ERR_HIP;
+                prep(c, sc);
+                if (stagger == 1 && hipEventRecord(pe[c], sc) != hipSuccess) return PP_ERR_HIP;
+                const int64_t g0 = g_lo(c), g1 = g_lo(c + 1);
+                if (g1 > g0) {
+                    hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sc, mg, B, P, pv, R,
+                                       cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
+                    hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)std::min<int64_t>(g1 - g0, 2048)), dim3(cg.threads), cg.lds, sc,
+                                       mg, B, P, pv, R, cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
+                }
+                if (stagger == 2 && hipEventRecord(pe[c], sc) != hipSuccess) return PP_ERR_HIP;
+                emit(c, sc);
+            }
+            if (hipEventRecord(e_done, ax) != hipSuccess || hipStreamWaitEvent(st, e_done, 0) != hipSuccess) return PP_ERR_HIP;
+            if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
+            if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+            return PP_OK;
+        }
+        for (int c = 0; c < 2 && c < nch; c++) { prep(c, ax); if (hipEventRecord(pe[c], ax) != hipSuccess) return PP_ERR_HIP; }
         for (int c = 0; c < nch; c++) {
             if (hipStreamWaitEvent(st, pe[c], 0) != hipSuccess) return PP_ERR_HIP;
             if (c == 0 && timing) (void)hipEventRecord(ev[1], st);
@@ -3338,8 +3372,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                                    mg, B, P, pv, R, cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
             }
             if (hipEventRecord(ce[c], st) != hipSuccess || hipStreamWaitEvent(ax, ce[c], 0) != hipSuccess) return PP_ERR_HIP;
-            emit(c);
-            if (c + 2 < nch) { prep(c + 2); if (hipEventRecord(pe[c + 2], ax) != hipSuccess) return PP_ERR_HIP; }
+            emit(c, ax);
+            if (c + 2 < nch) { prep(c + 2, ax); if (hipEventRecord(pe[c + 2], ax) != hipSuccess) return PP_ERR_HIP; }
         }
         if (timing) (void)hipEventRecord(ev[2], st);
         if (hipEventRecord(e_done, ax) != hipSuccess || hipStreamWaitEvent(st, e_done, 0) != hipSuccess) return PP_ERR_HIP;
