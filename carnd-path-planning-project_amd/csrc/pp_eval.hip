@@ -211,6 +211,9 @@ __device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int N
 #define PP_CAR_SORT_BATCH 0
 #endif
 // standing candidates (speed 0) take the turn series whatever the angle
+#ifndef PP_ROT_IDENT            // output-frame turns by Taylor + angle difference (run_candidate; measured slower)
+#define PP_ROT_IDENT 0
+#endif
 #ifndef PP_STAND_SERIES
 #define PP_STAND_SERIES 0
 #endif
@@ -1585,6 +1588,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
+        const double cr_st = cr, dt_st = dt;     // the turn's sine and cosine (curvature adjustment)
 #if PP_STEP_FAST
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
@@ -1671,7 +1675,29 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     tpy = tpy + cy;
                     const double vx = cx - tpx, vy = cy - tpy;
                     double cr, sr;
+#ifdef PP_ABL_CAND_TRIG     // diagnostic timing build (wrong results): first-order sin/cos of the turn
+                    sr = rot; cr = 1.0;
+#else
+#if PP_ROT_IDENT && PP_ANGLE_CROSS && PP_STEP_FAST
+                    // rot = nad - adiff. (cos adiff, sin adiff) = (u_prev . u, u_prev x u) are at hand
+                    // (adiff is their atan2, wrapped into [-pi, pi]). For |nad| <= 0.0709 (every
+                    // adjustment of a step faster than 2.3 m/s: |nad| = nc / (50 speed), nc <= 8)
+                    // cos/sin of nad come from their Taylor polynomials (through x^8 / x^9: below
+                    // 1e-19 there), then the angle-difference formulas give cos/sin of rot within a
+                    // few ulp (the output frame only). Otherwise (and in k_cand<true>)
+                    // the library's sin/cos of rot; NaN/inf nad (speed 0) takes that path too.
+                    if (!kLarge && fabs(nad) <= 0.0709) {
+                        const double x2 = nad * nad;
+                        const double sn = __builtin_fma(nad * x2, __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2,
+                                              1.0 / 362880, -1.0 / 5040), 1.0 / 120), -1.0 / 6), nad);
+                        const double cn = __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2,
+                                              1.0 / 40320, -1.0 / 720), 1.0 / 24), -0.5), 1.0);
+                        cr = cn * dt_st + sn * cr_st;
+                        sr = sn * dt_st - cn * cr_st;
+                    } else
+#endif
                     ppm::sincos_pp<kLarge>(rot, sr, cr);
+#endif
                     const double rvx = vx * cr - vy * sr;
                     const double rvy = vx * sr + vy * cr;
                     cx = tpx + rvx;
