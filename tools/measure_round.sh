@@ -16,12 +16,12 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke.log
 bash tools/pmc.sh $OUT/pmc
 python3 tools/pmc_summarize.py $OUT/pmc k_cand_S2097152_C15_N50 > $OUT/pmc_summary.txt
-bash tools/pmc.sh $OUT/pmc3 --steps 2 --warmup 1 --no-cpu-baseline --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
+bash tools/pmc.sh $OUT/pmc3 --steps 2 --warmup 1 --no-cpu-baseline --no-pcie --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
 python3 tools/pmc_summarize.py $OUT/pmc3 k_cand_S262144_C24_N100_paths > $OUT/pmc3_summary.txt
 cp profiles/pmc_summary.json $OUT/pmc_summary.json
 timeout -k 10 400 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
 tail -1 $OUT/bench.json | cut -c1-300
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/stats -o run -- python3 $ROOT/bench.py --no-cpu-baseline > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/stats -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-pcie > $OUT/bench_under_rocprof.json 2> $OUT/rocprof.err
 echo "rocprof done"
 run() { name=$1; shift; timeout -k 10 300 python3 bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err; echo "$name: $(tail -1 $OUT/$name.json | cut -c1-200)"; }
 run bench_config2 --scenes 4096 --steps 300 --warmup 30 --no-cpu-baseline

@@ -5,7 +5,7 @@
 set -e
 OUT=${1:-gpurun_out/pmc}
 shift || true
-ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline}
+ARGS=${@:---steps 2 --warmup 1 --no-cpu-baseline --no-pcie}
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
