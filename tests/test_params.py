@@ -1,0 +1,80 @@
+"""pp_params beyond the reference's constants (src/main.cpp:39-49 hard-codes relaxed_acc,
+maximum_acc, max_speed, car_length, safety_distance, keep_distance; include/pp.h makes them
+parameters). The reference cannot run these sets, so the oracle restatement, pinned at the
+defaults by the golden vectors, is the checker. Parity is unpinned against the reference
+itself for non-default values. On the GPU the HIP path must equal the oracle under the strict
+contract (oracle_lib.compare). k_prep's range proofs for the unchecked divisions depend on
+speeds and ramp times, so the sets move those: a lower and a higher acceleration limit, slower and
+faster speed caps, shorter and longer horizons, other grids, and both cost modes. Each set also
+checks that the paths-free (bench) evaluation equals the all-paths one."""
+import numpy as np
+import pytest
+
+import oracle_lib
+from oracle_lib import ppamd
+
+SETS = {
+    "soft_acc": dict(relaxed_acc=3.0, min_relaxed_acc_while_braking=2.5, maximum_acc=5.0),
+    "hard_acc": dict(relaxed_acc=8.0, min_relaxed_acc_while_braking=6.0, maximum_acc=12.0),
+    "slow_cap_short": dict(max_speed=15.0, n_points=30, n_speeds=3, speed_offsets=[-3.0, 1.0]),
+    "fast_cap_long": dict(max_speed=27.0, n_points=100, n_speeds=8, speed_offsets=[-6, -4, -3, -2, -1, 0, 2]),
+    "spacing": dict(car_length=6.0, safety_distance=4.0, keep_distance=25.0, keep_distance_leeway=2.0),
+    "comfort_hard": dict(maximum_acc=10.0, cost_mode=ppamd.COST_COMFORT, n_speeds=4, speed_offsets=[-5, -1, 3]),
+}
+
+
+def make_params(emit_paths, kw):
+    kw = dict(kw)
+    p = ppamd.default_params(n_speeds=kw.pop("n_speeds", 5), n_points=kw.pop("n_points", 50),
+                             cost_mode=kw.pop("cost_mode", ppamd.COST_REFERENCE), emit_paths=emit_paths,
+                             speed_offsets=kw.pop("speed_offsets", None))
+    for k, v in kw.items():
+        setattr(p, k, float(v))
+    return p
+
+
+def test_param_sets_are_valid_for_the_oracle():
+    """CPU: every set runs through the oracle (no parameter is rejected), and the sets do change the
+    decisions against the defaults on the same scenes."""
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    olib = oracle_lib.load_oracle()
+    host = ppamd.synth_host(m, 200, seed=31, first=9_000_000)
+    base = oracle_lib.oracle_eval(olib, wx, wy, host, make_params(True, {}), info=False)
+    changed = 0
+    for name, kw in SETS.items():
+        r = oracle_lib.oracle_eval(olib, wx, wy, host, make_params(True, kw), info=False)
+        assert r["n_out"].shape == (200,), name
+        changed += int(not np.array_equal(r["status"], base["status"]) or
+                       not np.allclose(r["next_x"], base["next_x"], equal_nan=True))
+    assert changed == len(SETS)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SETS))
+def test_param_set_vs_oracle(name):
+    import torch
+    kw = SETS[name]
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    olib = oracle_lib.load_oracle()
+    S = 3000
+    host = ppamd.synth_host(m, S, seed=101, first=7_000_000 + 10_000 * list(SETS).index(name))
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in host.items()}
+    out = {}
+    for paths in (True, False):
+        prm = make_params(paths, kw)
+        r = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
+        ppamd.evaluate(m, dev, prm, r, device=0)
+        torch.cuda.synchronize()
+        out[paths] = ppamd.result_to_numpy(r)
+    ref = oracle_lib.oracle_eval(olib, wx, wy, host, make_params(True, kw), info=False)
+    e = oracle_lib.compare(out[True], ref)
+    got, got_e = out[False], out[True]
+    np.testing.assert_array_equal(got["cost"], got_e["cost"])
+    for k in ("winner", "n_out", "status"):
+        assert np.array_equal(got[k], got_e[k]), (name, k)
+    for k in ("next_x", "next_y"):
+        e = max(e, oracle_lib.max_err(got[k], got_e[k]))
+    assert e <= oracle_lib.TOL, (name, e)
+    print(f"{name}: max |dxy| {e:.3e} m")
