@@ -2168,6 +2168,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 
                                               uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
                                               const uint32_t* gcount, int64_t g0) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
+#ifndef PP_PRIO
+#define PP_PRIO 0
+#endif
+    // PP_PRIO (experiment): issue priority of the block's first wave, which carries the serial
+    // phase-A steps and the winners' longer recording body that the block's LDS waits for
+    if (PP_PRIO > 0 && threadIdx.x < 64) __builtin_amdgcn_s_setprio(PP_PRIO);
     if (!kSlow) {
         cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g0 + blockIdx.x, sm);
         return;
