@@ -20,7 +20,15 @@ SETS = {
     "fast_cap_long": dict(max_speed=27.0, n_points=100, n_speeds=8, speed_offsets=[-6, -4, -3, -2, -1, 0, 2]),
     "spacing": dict(car_length=6.0, safety_distance=4.0, keep_distance=25.0, keep_distance_leeway=2.0),
     "comfort_hard": dict(maximum_acc=10.0, cost_mode=ppamd.COST_COMFORT, n_speeds=4, speed_offsets=[-5, -1, 3]),
+    # horizon limits: 11 points (one beyond the 10 kept), 127 (the fused small-batch kernels' last
+    # size), PP_MAX_POINTS = 128 (adjusted-step masks in both 64-bit words)
+    "horizon_11": dict(n_points=11),
+    "horizon_127": dict(n_points=127, max_speed=27.0),
+    "horizon_128": dict(n_points=128, max_speed=27.0),
 }
+# scenes per set: 3,000 take the fused small-batch kernels where N <= 127 (k_step_small / k_cand_small);
+# 20,000 at N = 128 take k_prep + k_cand + k_emit
+SIZES = {"horizon_128": 20000}
 
 
 def make_params(emit_paths, kw):
@@ -58,7 +66,7 @@ def test_param_set_vs_oracle(name):
     wx, wy = oracle_lib.highway_map()
     m = ppamd.Map(wx, wy)
     olib = oracle_lib.load_oracle()
-    S = 3000
+    S = SIZES.get(name, 3000)
     host = ppamd.synth_host(m, S, seed=101, first=7_000_000 + 10_000 * list(SETS).index(name))
     dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in host.items()}
     out = {}
@@ -78,3 +86,19 @@ def test_param_set_vs_oracle(name):
         e = max(e, oracle_lib.max_err(got[k], got_e[k]))
     assert e <= oracle_lib.TOL, (name, e)
     print(f"{name}: max |dxy| {e:.3e} m")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_points", [10, ppamd.MAX_POINTS + 1])
+def test_horizon_out_of_range_rejected(n_points):
+    """N must exceed the 10 kept points and stay <= PP_MAX_POINTS: PP_ERR_ARG, nothing launched"""
+    import torch
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    host = ppamd.synth_host(m, 64, seed=3)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in host.items()}
+    prm = make_params(False, dict(n_points=n_points))
+    r = ppamd.alloc_result(64, make_params(False, dict(n_points=min(n_points, ppamd.MAX_POINTS))),
+                           xp="torch", device=torch.device("cuda", 0))
+    with pytest.raises(ppamd.PPError):
+        ppamd.evaluate(m, dev, prm, r, device=0)
