@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -98,3 +99,30 @@ def test_launcher_starts_n_ranks():
                                   ppamd.default_params(), info=False)
     parts = [float(np.nansum(full["cost"][f:f + n])) for f, n in out["shards"]]
     assert np.allclose(parts, out["cost_digests"], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_launcher_two_ranks_on_the_gpu():
+    """`bench.py --gpus 2` on the GPU box: two rank processes (more ranks than GPUs share them), the
+    strong-scaling shards of one batch, gloo barrier + MAX, the PCIe leg on every rank, and the
+    weak-scaling side measurement; rank 0 reports n_gpus = 2 and both ranks' kernel times."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(oracle_lib.REPO, "bench.py"), "--gpus", "2", "--scenes", "65536",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--pcie-chunks", "2"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["value"] > 0
+    ranks = out["per_rank_kernels_ms"]
+    assert [x["rank"] for x in ranks] == [0, 1] and [x["scenes"] for x in ranks] == [32768, 32768]
+    assert all(x["k_cand"] > 0 for x in ranks)
+    assert out["weak_scaling"]["scenes_per_gpu"] == bench_config5() and out["weak_scaling"]["value"] > 0
+    assert out["pcie_inclusive"]["value"] > 0, out["pcie_inclusive"]
+
+
+def bench_config5():
+    import bench
+    return bench.CONFIG5_SCENES
