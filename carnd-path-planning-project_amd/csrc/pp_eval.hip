@@ -1588,7 +1588,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
+#if PP_ROT_IDENT
         const double cr_st = cr, dt_st = dt;     // the turn's sine and cosine (curvature adjustment)
+#endif
 #if PP_STEP_FAST
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
@@ -2668,6 +2670,8 @@ struct DevState {
     double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
+    void* frame_host = nullptr;   // its pinned host staging copy
+    hipStream_t frame_stream = nullptr;  // pp_plan_frame's stream (copies and kernels, one sync)
     std::mutex frame_mu;          // one pp_plan_frame at a time per device (frame scratch + car table)
     void* stage = nullptr;        // pp_plan_batch_host staging buffer
     size_t stage_cap = 0;
@@ -3188,6 +3192,8 @@ int32_t pp_map_destroy(pp_map* M) {
         for (auto& kv : D.sws) free_ws(kv.second);
         D.sws.clear();
         if (D.frame) (void)hipFree(D.frame);
+        if (D.frame_host) (void)hipHostFree(D.frame_host);
+        if (D.frame_stream) (void)hipStreamDestroy(D.frame_stream);
         if (D.stage) (void)hipFree(D.stage);
         for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : D.ev_rec) (void)hipEventDestroy(e);
@@ -3782,7 +3788,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     }
     std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.id < b.id; });
     const int nc = (int)rows.size();
-    // device scratch layout (bytes): doubles then ints
+    // device scratch layout (bytes): doubles then ints, then the scene info (the target lane)
     constexpr int N = 50;
     constexpr int TS = PP_MAX_CARS;
     struct Frame {
@@ -3793,8 +3799,24 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         int32_t tid[TS], tvalid[TS], tlane[TS];
         int32_t nprev, ptl, ncars, cid[PP_MAX_CARS], winner, nout;
         uint32_t status;
+        pp_scene_info info;
     };
-    Frame h;
+    DeviceGuard g(device);
+    std::lock_guard<std::mutex> frame_lock(M->dev[device].frame_mu);
+    DevState& DS = M->dev[device];
+    Frame* d = nullptr;
+    {   // per-device scratch, made once: the device frame, its pinned host copy, the frame stream
+        std::lock_guard<std::mutex> lk(M->mu);
+        int rc = dev_init(M, device);
+        if (rc) return rc;
+        if (!DS.frame && hipMalloc(&DS.frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
+        if (!DS.frame_host && hipHostMalloc(&DS.frame_host, sizeof(Frame), hipHostMallocDefault) != hipSuccess)
+            return PP_ERR_NOMEM;
+        if (!DS.frame_stream && hipStreamCreateWithFlags(&DS.frame_stream, hipStreamNonBlocking) != hipSuccess)
+            return PP_ERR_HIP;
+        d = (Frame*)DS.frame;
+    }
+    Frame& h = *(Frame*)DS.frame_host;
     memset(&h, 0, sizeof(h));
     h.ego[0] = ego_x; h.ego[1] = ego_y; h.ego[2] = ego_yaw_deg; h.ego[3] = ego_speed_mph;
     for (int i = 0; i < PP_PREV_KEEP && i < n_prev; i++) { h.px[i] = prev_x[i]; h.py[i] = prev_y[i]; }
@@ -3802,22 +3824,12 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     for (int j = 0; j < nc; j++) {
         h.cid[j] = rows[j].id; h.cx[j] = rows[j].x; h.cy[j] = rows[j].y; h.cvx[j] = rows[j].vx; h.cvy[j] = rows[j].vy;
     }
-    DeviceGuard g(device);
-    std::lock_guard<std::mutex> frame_lock(M->dev[device].frame_mu);
-    DevState& DS = M->dev[device];
     // the reference's std::map, laid out over the union of its ids and this frame's (any ints)
     const pptab::Slots hs = {1, h.tid, h.tvalid, h.tlane, h.ts, h.td, h.tvs, h.tvd, h.tvx, h.tvy};
     const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS);
     if (nslots < 0) return PP_ERR_ARG;                  // more than PP_MAX_CARS distinct cars
-    Frame* d = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(M->mu);
-        int rc = dev_init(M, device);
-        if (rc) return rc;
-        if (!DS.frame && hipMalloc(&DS.frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
-        d = (Frame*)DS.frame;
-    }
-    if (hipMemcpy(d, &h, sizeof(Frame), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
+    hipStream_t st = DS.frame_stream;
+    if (hipMemcpyAsync(d, &h, sizeof(Frame), hipMemcpyHostToDevice, st) != hipSuccess) return PP_ERR_HIP;
     pp_scene_batch B;
     memset(&B, 0, sizeof(B));
     B.n_scenes = 1; B.car_stride = PP_MAX_CARS;
@@ -3830,23 +3842,20 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     pp_params P;
     pp_params_default(&P);
     P.n_speeds = 1;
-    pp_scene_info* dinfo = nullptr;
-    if (hipMalloc(&dinfo, sizeof(pp_scene_info)) != hipSuccess) return PP_ERR_NOMEM;
     pp_result R;
     memset(&R, 0, sizeof(R));
     R.winner = &d->winner; R.n_out = &d->nout; R.next_x = d->nx; R.next_y = d->ny; R.cost = d->cost;
-    R.status = &d->status; R.info = dinfo;
-    int rc = pp_eval(M, &B, &P, &R, device, nullptr);
-    if (rc == PP_OK && hipDeviceSynchronize() != hipSuccess) rc = PP_ERR_HIP;
-    pp_scene_info hi;
-    if (rc == PP_OK && hipMemcpy(&h, d, sizeof(Frame), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
-    if (rc == PP_OK && hipMemcpy(&hi, dinfo, sizeof(hi), hipMemcpyDeviceToHost) != hipSuccess) rc = PP_ERR_HIP;
-    (void)hipFree(dinfo);
+    R.status = &d->status; R.info = &d->info;
+    int rc = pp_eval(M, &B, &P, &R, device, (void*)st);
+    // one copy back (plan, car table, scene info) and one synchronisation of the frame's stream
+    if (rc == PP_OK && (hipMemcpyAsync(&h, d, sizeof(Frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipStreamSynchronize(st) != hipSuccess))
+        rc = PP_ERR_HIP;
     if (rc != PP_OK) return rc;
     DS.plan_table.take_back(hs, 0, nslots);
     *n_out = h.nout;
     for (int i = 0; i < h.nout && i < N; i++) { next_x[i] = h.nx[i]; next_y[i] = h.ny[i]; }
-    *target_lane = hi.target_lane;
+    *target_lane = h.info.target_lane;
     return PP_OK;
 }
 
