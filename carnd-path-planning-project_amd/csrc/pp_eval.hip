@@ -980,25 +980,55 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
     a.init();
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
+    // Without a car table: the frame's rows. With one (the reference's persistent std::map, as
+    // k_prep): its tab_slots slots in order, each either reported this frame (re-matched; the slot
+    // overwritten, or erased when matching fails, src/main.cpp:1329-1348) or taken from its stale
+    // slot. Iteration index = row or slot, as in k_prep.
+    const bool tab = in.tab_valid != nullptr;
+    const int iters = tab ? in.tab_slots : ncar;
     uint32_t ust = 0;
-    for (int j0 = 0; j0 < ncar; j0 += G) {
+    for (int j0 = 0; j0 < iters; j0 += G) {
         const int j = j0 + r;
         int okl = 0, id = 0;                  // okl: matched | lane << 1
         double cs = 0, cd = 0, cvs = 0, cvd = 0;
-        if (j < ncar) {
-            const int64_t ix = (int64_t)j * S + s;
-            id = in.car_id[ix];
-            double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
-            if (draw > 0) car_noise(P, s, draw, j, cx, cy, cvx, cvy);
-            int nwp = 0, clane = 0;
-            if (lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
-                project_speed(m, cvx, cvy, nwp, cvs, cvd);
-                okl = 1 | (clane << 1);
-            } else {
-                ust |= PP_ST_CAR_UNMATCHED;
+        if (j < iters) {
+            const int64_t tix = (int64_t)j * S + s;
+            int row = j;
+            if (tab) {
+                // slot j holds id sid; its reported row, if any (rows ascend by id: the first row
+                // with that id, the row k_prep's merge pointer reaches)
+                const int sid = in.tab_id ? in.tab_id[tix] : j;
+                row = -1;
+                for (int p = 0; p < ncar; p++) {
+                    const int cid = in.car_id[(int64_t)p * S + s];
+                    if (cid >= sid) { if (cid == sid) row = p; break; }
+                }
+                id = sid;
+            }
+            if (row >= 0) {
+                const int64_t ix = (int64_t)row * S + s;
+                id = in.car_id[ix];
+                double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+                if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
+                int nwp = 0, clane = 0;
+                if (lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
+                    project_speed(m, cvx, cvy, nwp, cvs, cvd);
+                    okl = 1 | (clane << 1);
+                    if (tab) {
+                        in.tab_valid[tix] = 1; in.tab_lane[tix] = clane;
+                        in.tab_s[tix] = cs; in.tab_d[tix] = cd; in.tab_vs[tix] = cvs; in.tab_vd[tix] = cvd;
+                        in.tab_vx[tix] = cvx; in.tab_vy[tix] = cvy;
+                    }
+                } else {
+                    ust |= PP_ST_CAR_UNMATCHED;
+                    if (tab) in.tab_valid[tix] = 0;
+                }
+            } else if (in.tab_valid[tix]) {   // (tab only) a stale slot
+                okl = 1 | (in.tab_lane[tix] << 1);
+                cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
             }
         }
-        const int nq = ncar - j0 < G ? ncar - j0 : G;
+        const int nq = iters - j0 < G ? iters - j0 : G;
         for (int q = 0; q < nq; q++) {
             const int qokl = __shfl(okl, q, G);
             const int qid = __shfl(id, q, G);
@@ -1008,7 +1038,10 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
         }
     }
     status |= grp_or<G>(ust);
-    prep_finish<G>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, false, r, T_in, e, a, status);
+    // prep_finish re-reads the follow cars' velocities from the slots other lanes of the group
+    // (same wave) wrote above
+    if (tab) __threadfence_block();
+    prep_finish<G>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, r, T_in, e, a, status);
 }
 
 // the grouped instantiations by name (pp_eval's launch switch)
@@ -3318,6 +3351,8 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const int64_t groups_f = (S + spb_f - 1) / spb_f;
     const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * mg.n + 1) & ~1);
     const size_t lds_f = map_lds + cand_geom_lds(spb_f);
+    // (car tables: the grouped K1 in its own kernel; inside k_step_small the closed-loop replays
+    // diverged from the reference, so that combination is not used)
     const bool step_fused = fused && !B.tab_valid && mg.n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
     if (step_fused) {
         if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
@@ -3424,7 +3459,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
         const int threads = 256;
-        const int G = B.tab_valid ? 1 : prep_group(Sv);
+        const int G = prep_group(Sv);
         const int64_t blocks = (Sv * G + threads - 1) / threads;
         if (timing) (void)hipEventRecord(ev[0], st);
 #ifdef PP_PREP_GMAP   // diagnostic timing build: k_prep reads the map through L1/L2 at any size

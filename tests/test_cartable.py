@@ -202,3 +202,49 @@ class TestCarTableGPU:
         print(f"ids {ids[:3]}..: max |dxy| {worst:.3e} m, frames with stale entries {stale}, "
               f"with erased {erased}, max reported {rep}")
         assert (stale if need == "stale" else erased) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 37, 600, 5000])
+def test_table_mode_group_invariance(S):
+    """Car-table mode through K1 with G = 1 (one lane per scene) and G = 2..16 (the grouped K1: slots
+    split over the group, planner in slot order): the same outputs and the same updated table, bit
+    for bit. The table state has reported, stale and erased slots: a first frame fills it, the
+    second reports only some of the cars (the others stay as stale slots)."""
+    import torch
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    dev = torch.device("cuda", 0)
+    host = ppamd.synth_host(m, S, seed=515, first=3_000_000)
+    prm = ppamd.default_params(emit_paths=True)
+
+    def to_dev(d):
+        return {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+
+    sc = ppamd.add_car_table(dict(host), slots=12)
+    d0 = to_dev(sc)
+    r = ppamd.alloc_result(S, prm, xp="torch", device=dev)
+    ppamd.set_prep_group(1)
+    try:
+        ppamd.evaluate(m, d0, prm, r, device=0)          # frame 1 fills the table
+        torch.cuda.synchronize()
+        state = {k: v.cpu().numpy() for k, v in d0.items()}
+        rng = np.random.default_rng(S)
+        state["n_cars"] = rng.integers(0, 13, S).astype(np.int32)   # frame 2 reports a prefix of the rows
+        outs = {}
+        for G in (1, 2, 4, 8, 16):
+            ppamd.set_prep_group(G)
+            d = to_dev(state)
+            rr = ppamd.alloc_result(S, prm, xp="torch", device=dev)
+            ppamd.evaluate(m, d, prm, rr, device=0)
+            torch.cuda.synchronize()
+            outs[G] = ({k: v for k, v in ppamd.result_to_numpy(rr).items()},
+                       {k: d[k].cpu().numpy() for k in ppamd.TABLE_FIELDS_I + ppamd.TABLE_FIELDS_F})
+    finally:
+        ppamd.set_prep_group(0)
+    assert (state["tab_valid"].sum(0) > state["n_cars"]).any()      # stale slots present
+    for G in (2, 4, 8, 16):
+        for k, v in outs[1][0].items():
+            assert np.array_equal(np.ascontiguousarray(v).view(np.uint8), np.ascontiguousarray(outs[G][0][k]).view(np.uint8)), (G, k)
+        for k, v in outs[1][1].items():
+            assert np.array_equal(v.view(np.uint8), outs[G][1][k].view(np.uint8)), (G, k)
