@@ -2708,6 +2708,7 @@ struct DevState {
     std::mutex frame_mu;          // one pp_plan_frame at a time per device (frame scratch + car table)
     void* stage = nullptr;        // pp_plan_batch_host staging buffer
     size_t stage_cap = 0;
+    void* stage_host = nullptr;   // its pinned host mirror (one copy per direction and region)
     std::mutex stage_mu;          // one pp_plan_batch_host at a time per device
     pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
     bool timing = false;          // pp_timing_enable
@@ -3228,6 +3229,7 @@ int32_t pp_map_destroy(pp_map* M) {
         if (D.frame_host) (void)hipHostFree(D.frame_host);
         if (D.frame_stream) (void)hipStreamDestroy(D.frame_stream);
         if (D.stage) (void)hipFree(D.stage);
+        if (D.stage_host) (void)hipHostFree(D.stage_host);
         for (hipEvent_t e : D.ev_pool) (void)hipEventDestroy(e);
         for (hipEvent_t e : D.ev_rec) (void)hipEventDestroy(e);
     }
@@ -3690,6 +3692,8 @@ int32_t pp_rollout(pp_map* M, pp_scene_batch* tel, pp_traffic* traffic, const pp
 
 // Host-memory batch (the batched onMessage): stage the scenes (and their car table) into device
 // memory, pp_eval, copy results (and the updated table) back. Synchronous.
+// pp_plan_batch_host stages batches up to this many scenes through its pinned mirror
+constexpr int64_t kStageMirrorMax = 512;
 int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const pp_params* prm,
                            pp_result* hout, void* hip_stream) {
     if (!M || !hin || !prm || !hout || device < 0 || device >= kMaxDev || !params_ok(prm) || prm->emit_paths ||
@@ -3712,6 +3716,7 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     hipStream_t st = (hipStream_t)hip_stream;
     std::lock_guard<std::mutex> stage_lock(M->dev[device].stage_mu);
     char* base;
+    char* mirror;                 // pinned host mirror of the staging buffer (same offsets)
     {
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
@@ -3719,18 +3724,30 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
         DevState& D = M->dev[device];
         if (D.stage_cap < bytes) {
             if (D.stage) { (void)hipDeviceSynchronize(); (void)hipFree(D.stage); D.stage = nullptr; D.stage_cap = 0; }
+            if (D.stage_host) { (void)hipHostFree(D.stage_host); D.stage_host = nullptr; }
             if (hipMalloc(&D.stage, bytes) != hipSuccess) return PP_ERR_NOMEM;
+            if (hipHostMalloc(&D.stage_host, bytes, hipHostMallocDefault) != hipSuccess) {
+                (void)hipFree(D.stage); D.stage = nullptr; return PP_ERR_NOMEM;
+            }
             D.stage_cap = bytes;
         }
         base = (char*)D.stage;
+        mirror = (char*)D.stage_host;
     }
     double* dp = (double*)base;
     int32_t* ip = (int32_t*)(base + nd * 8);
     auto takeD = [&](size_t n) { double* r = dp; dp += n; return r; };
     auto takeI = [&](size_t n) { int32_t* r = ip; ip += n; return r; };
     bool ok = true;
+    // Small batches (latency): inputs are gathered into the pinned mirror; the input fields lead
+    // each region (doubles, then ints), so one copy per region moves them, and one per region
+    // brings the outputs back. Large batches (bandwidth): one asynchronous copy per field straight
+    // from and to the caller's buffers (the extra host memcpy through the mirror costs more there).
+    const bool small = S <= kStageMirrorMax;
     auto h2d = [&](void* d, const void* h, size_t n) {
-        if (n && hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st) != hipSuccess) ok = false;
+        if (!n) return;
+        if (small) memcpy(mirror + ((char*)d - base), h, n);
+        else if (hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st) != hipSuccess) ok = false;
     };
     pp_scene_batch B;
     memset(&B, 0, sizeof(B));
@@ -3776,11 +3793,31 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     memset(&R, 0, sizeof(R));
     R.winner = outi; R.n_out = outi + S; R.status = (uint32_t*)(outi + 2 * S);
     R.next_x = nxy; R.next_y = nxy + (size_t)N * S; R.cost = cost;
+    const char* d_in_end = (const char*)nxy;           // doubles: inputs [base, nxy)
+    const char* i_beg = base + nd * 8;                  // ints: inputs [i_beg, outi)
+    const char* d_out_beg = tab ? (const char*)tabd : (const char*)nxy;   // outputs: (tables,) plans, costs
+    const char* d_out_end = (const char*)(cost + (size_t)C * S);
+    const char* i_out_beg = tab ? (const char*)tabi : (const char*)outi;
+    const char* i_out_end = (const char*)(outi + 3 * S);
+    auto copy = [&](const char* lo, const char* hi, bool in) {
+        if (hi <= lo) return;
+        char* h = mirror + (lo - base);
+        if (hipMemcpyAsync(in ? (void*)lo : (void*)h, in ? (const void*)h : (const void*)lo, (size_t)(hi - lo),
+                           in ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, st) != hipSuccess) ok = false;
+    };
+    if (small) { copy(base, d_in_end, true); copy(i_beg, (const char*)outi, true); }
     if (!ok) return PP_ERR_HIP;
     int rc = pp_eval(M, &B, prm, &R, device, hip_stream);
     if (rc != PP_OK) return rc;
+    if (small) {
+        copy(d_out_beg, d_out_end, false);
+        copy(i_out_beg, i_out_end, false);
+        if (!ok || hipStreamSynchronize(st) != hipSuccess) return PP_ERR_HIP;
+    }
     auto d2h = [&](void* h, const void* d, size_t n) {
-        if (n && hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) ok = false;
+        if (!n) return;
+        if (small) memcpy(h, mirror + ((const char*)d - base), n);
+        else if (hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, st) != hipSuccess) ok = false;
     };
     d2h(hout->winner, R.winner, 4 * S); d2h(hout->n_out, R.n_out, 4 * S); d2h(hout->status, R.status, 4 * S);
     d2h(hout->next_x, R.next_x, 8 * (size_t)N * S); d2h(hout->next_y, R.next_y, 8 * (size_t)N * S);
@@ -3790,7 +3827,7 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
         for (int k = 0; k < 6; k++) d2h(dstd[k], tabd + k * (size_t)TS * S, 8 * (size_t)TS * S);
         d2h(hin->tab_valid, tabi, 4 * (size_t)TS * S); d2h(hin->tab_lane, tabi + (size_t)TS * S, 4 * (size_t)TS * S);
     }
-    if (!ok || hipStreamSynchronize(st) != hipSuccess) return PP_ERR_HIP;
+    if (!small && (!ok || hipStreamSynchronize(st) != hipSuccess)) return PP_ERR_HIP;
     return PP_OK;
 }
 
