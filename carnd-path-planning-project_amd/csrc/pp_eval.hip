@@ -3353,12 +3353,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const int64_t groups_f = (S + spb_f - 1) / spb_f;
     const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * mg.n + 1) & ~1);
     const size_t lds_f = map_lds + cand_geom_lds(spb_f);
-    // (car tables: the grouped K1 in its own kernel; inside k_step_small the closed-loop replays
-    // diverged from the reference, so that combination is not used)
-    const bool step_fused = fused && !B.tab_valid && mg.n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
+    const bool step_fused = fused && mg.n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
     if (step_fused) {
         if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
-        hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(cg.threads), lds_f, st, mg, B, P, pv,
+        // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
+        // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
+        const int threads_f = std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
+        hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
                            R, spb_f, rec, adjm);
         if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;

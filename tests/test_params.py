@@ -102,3 +102,27 @@ def test_horizon_out_of_range_rejected(n_points):
                            xp="torch", device=torch.device("cuda", 0))
     with pytest.raises(ppamd.PPError):
         ppamd.evaluate(m, dev, prm, r, device=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_speeds", [1, 2, 3])
+def test_small_grid_fresh_batch_vs_oracle(n_speeds):
+    """Small batches with C = 3, 6, 9 candidates per scene (k_step_small, whose block must hold 16
+    K1 lanes per scene beside the C lanes per scene of K2). Each batch follows a different batch of
+    the same size on the same stream, so no scene can reuse a prep record the previous call left in
+    the workspace."""
+    import torch
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    olib = oracle_lib.load_oracle()
+    S = 700
+    prm = make_params(False, dict(n_speeds=n_speeds, speed_offsets=[-3.0, -1.0][:n_speeds - 1]))
+    for first in (11_000_000, 12_000_000):
+        host = ppamd.synth_host(m, S, seed=7, first=first)
+        dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to("cuda:0") for k, v in host.items()}
+        r = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
+        ppamd.evaluate(m, dev, prm, r, device=0)
+        torch.cuda.synchronize()
+    got = ppamd.result_to_numpy(r)
+    ref = oracle_lib.oracle_eval(olib, wx, wy, host, prm, info=False)
+    oracle_lib.compare(got, ref)
