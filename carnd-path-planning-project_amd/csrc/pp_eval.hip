@@ -3307,6 +3307,15 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         rec = rec_buf(W.rec);
         adjm = adj_buf(W.rec, W.rec_cap);
     }
+    {   // PP_POISON_WS=1 (test builds' switch, read once): every call starts from a NaN-filled prep
+        // workspace and winner record, so no kernel can lean on what an earlier call left there
+        static const bool poison = [] { const char* e = getenv("PP_POISON_WS"); return e && *e == '1'; }();
+        if (poison) {
+            if (hipMemsetAsync(W.ws, 0xFF, prep_bytes(W.ws_cap), st) != hipSuccess) return PP_ERR_HIP;
+            if (rec && hipMemsetAsync(rec, 0xFF, sizeof(double) * 3 * PP_MAX_POINTS * (size_t)W.rec_cap, st) != hipSuccess)
+                return PP_ERR_HIP;
+        }
+    }
     const PrepV pv = prep_bind(W.ws, W.ws_cap);
     MapG mg;
     mg.buf = DS.map;
