@@ -999,7 +999,11 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
                 // with that id, the row k_prep's merge pointer reaches)
                 const int sid = in.tab_id ? in.tab_id[tix] : j;
                 row = -1;
-                for (int p = 0; p < ncar; p++) {
+                // slot ids ascend strictly; a slot repeating its predecessor's id is padding
+                // (pp_cartable.h pads with INT32_MAX, which may also be a real car's id): it
+                // matches no row, as k_prep's merge pointer has already passed that row
+                const bool pad = in.tab_id && j > 0 && in.tab_id[tix - S] >= sid;
+                for (int p = pad ? ncar : 0; p < ncar; p++) {
                     const int cid = in.car_id[(int64_t)p * S + s];
                     if (cid >= sid) { if (cid == sid) row = p; break; }
                 }
@@ -3719,6 +3723,15 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     // staging layout: doubles first, then 4-byte fields
     const int TS = tab ? hin->tab_slots : 0;
     if (tab && (TS < 0 || TS > PP_MAX_CARS)) return PP_ERR_ARG;
+    // every host pointer the staging copies touch (small batches memcpy them on the host, so a
+    // NULL here must be refused before staging, not left to the copy)
+    if (!hin->ego_x || !hin->ego_y || !hin->ego_yaw_deg || !hin->ego_speed_mph || !hin->prev_x || !hin->prev_y ||
+        !hin->n_prev || !hin->prev_target_lane || !hin->n_cars)
+        return PP_ERR_ARG;
+    if (J > 0 && (!hin->car_id || !hin->car_x || !hin->car_y || !hin->car_vx || !hin->car_vy)) return PP_ERR_ARG;
+    if (tab && TS > 0 && (!hin->tab_lane || !hin->tab_s || !hin->tab_d || !hin->tab_vs || !hin->tab_vd ||
+                          !hin->tab_vx || !hin->tab_vy))
+        return PP_ERR_ARG;
     const size_t nd = (size_t)S * (4 + 2 * PP_PREV_KEEP + 4 * J + 6 * TS + 2 * N + C);
     const size_t ni = (size_t)S * (3 + J + 3 * TS + 3);
     const size_t bytes = nd * 8 + ni * 4 + 256;

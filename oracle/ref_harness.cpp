@@ -46,14 +46,46 @@ static void apply_limits(std::map<int, Car>& cars, SpeedController& sc, int in_i
 
 }  // namespace refh
 
-// Outputs (all host, caller-allocated):
-//   ref_next [S][50][2], ref_n [S], ref_T [S]          : the reference frame's own trajectory
-//   paths [S][C][50][2] (NaN padded), path_len [S][C]  : every candidate (lane, speed)
+// The tunables of src/main.cpp:39-49 are mutable globals in the reference; ref_set_params assigns
+// them from a pp_params (include/pp.h, same names and meaning) so that non-default parameter sets
+// run through the reference's own classes. The horizon (n_points) is settable only in the build
+// whose :854/:1039 literals are replaced by ref_n_points (_ref/libppref_n.so, -DPP_REF_NVAR);
+// elsewhere any value but 50 is refused (-1). Returns 0.
+extern "C" int ref_horizon_variable() {
+#ifdef PP_REF_NVAR
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+extern "C" int ref_set_params(const pp_params* p) {
+#ifdef PP_REF_NVAR
+    if (p->n_points <= PP_PREV_KEEP || p->n_points > PP_MAX_POINTS) return -1;
+#else
+    if (p->n_points != 50) return -1;
+#endif
+    ref_n_points = p->n_points;
+    relaxed_acc = p->relaxed_acc;                                        // :39-49
+    min_relaxed_acc_while_braking = p->min_relaxed_acc_while_braking;
+    maximum_acc = p->maximum_acc;
+    max_speed = p->max_speed;
+    car_length = p->car_length;
+    safety_distance = p->safety_distance;
+    keep_distance = p->keep_distance;
+    keep_distance_leeway = p->keep_distance_leeway;
+    return 0;
+}
+
+// Outputs (all host, caller-allocated; N = ref_n_points, 50 unless ref_set_params changed it):
+//   ref_next [S][N][2], ref_n [S], ref_T [S]           : the reference frame's own trajectory
+//   paths [S][C][N][2] (NaN padded), path_len [S][C]   : every candidate (lane, speed)
 //   info [S][8]: ego_s, ego_d, ego_vs, ego_vd, ego_speed, ego_acc, ego_lane, ref_wp
 extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_scene_batch* in,
                         int n_speeds, const double* speed_offsets, int with_frame,
                         double* ref_next, int* ref_n,
                         int* ref_T, double* paths, int* path_len, double* info) {
+    const int N = ref_n_points;
     Map map;
     vector<double> X(wx, wx + n_wp), Y(wy, wy + n_wp);
     map.Init(X, Y);
@@ -139,9 +171,9 @@ extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_s
                                                target_lane, ego_d, ego_vd, map, speed_controller);
             ref_n[s] = (int)r.size();
             ref_T[s] = target_lane;
-            for (int i = 0; i < 50; i++) {
-                ref_next[(s * 50 + i) * 2 + 0] = i < (int)r.size() ? r[i].x : 0.0;
-                ref_next[(s * 50 + i) * 2 + 1] = i < (int)r.size() ? r[i].y : 0.0;
+            for (int i = 0; i < N; i++) {
+                ref_next[(s * N + i) * 2 + 0] = i < (int)r.size() ? r[i].x : 0.0;
+                ref_next[(s * N + i) * 2 + 1] = i < (int)r.size() ? r[i].y : 0.0;
             }
         }
         // every candidate (lane L, speed k): SpeedController with target v (k = 0: max_speed)
@@ -165,11 +197,11 @@ extern "C" int ref_eval(const double* wx, const double* wy, int n_wp, const pp_s
             vector<Point> r = tb.build(prev_trajectory, ego_x, ego_y, ego_yaw, ego_lane, L, ego_d,
                                        ego_vd, map, sc);
             path_len[s * C + c] = (int)r.size();
-            for (int i = 0; i < 50; i++) {
+            for (int i = 0; i < N; i++) {
                 double px = i < (int)r.size() ? r[i].x : NAN;
                 double py = i < (int)r.size() ? r[i].y : NAN;
-                paths[((s * C + c) * 50 + i) * 2 + 0] = px;
-                paths[((s * C + c) * 50 + i) * 2 + 1] = py;
+                paths[((s * C + c) * N + i) * 2 + 0] = px;
+                paths[((s * C + c) * N + i) * 2 + 1] = py;
             }
         }
         double* I = info + s * 8;

@@ -21,3 +21,10 @@
 #include "spline.h"
 using std::string;
 using std::vector;
+
+// The horizon's point count. The reference hard-codes it as the literal 50 at src/main.cpp:854
+// (`result_points.size() < 50`) and :1039 (`>= 50`); _ref/libppref_n.so is built with exactly those
+// two literals replaced by this variable (oracle/Makefile), so ref_set_params can pin horizons other
+// than 50 to the reference's own code. The 50 m reach at :911 is a distance and stays as it lies.
+// In the builds without the substitution the variable only sizes the harness's output arrays.
+int ref_n_points = 50;

@@ -82,10 +82,14 @@ def draw_decision(cost, D, Cv):
     return mean, np.argmin(mean, axis=1).astype(np.int32)
 
 
-def load_ref():
-    if not os.path.exists(REF_SO):
+def load_ref(path=None):
+    path = path or REF_SO
+    if not os.path.exists(path):
         return None
-    lib = C.CDLL(REF_SO)
+    lib = C.CDLL(path)
+    lib.ref_set_params.argtypes = [C.POINTER(ppamd.Params)]
+    lib.ref_set_params.restype = C.c_int
+    lib.ref_horizon_variable.restype = C.c_int
     lib.ref_eval.argtypes = [_dp, _dp, C.c_int, C.POINTER(ppamd.SceneBatch), C.c_int, _dp, C.c_int, _dp,
                              C.POINTER(C.c_int), C.POINTER(C.c_int), _dp, C.POINTER(C.c_int), _dp]
     lib.ref_eval.restype = C.c_int
@@ -193,12 +197,32 @@ def oracle_eval(lib, wx, wy, scenes, prm, begin=0, end=None, info=True):
     return r
 
 
-def ref_eval(lib, wx, wy, scenes, n_speeds, speed_offsets, with_frame=True):
-    """Run the reference-compiled checker (N = 50 only: the reference hard-codes it)."""
+REF_N_SO = os.path.join(REPO, "oracle", "_ref", "libppref_n.so")
+
+
+def load_ref_n():
+    """The reference built with its two point-count literals (src/main.cpp:854, :1039) replaced by
+    a settable horizon (oracle/Makefile _ref/libppref_n.so), or None."""
+    lib = load_ref(REF_N_SO)
+    if lib is not None:
+        assert lib.ref_horizon_variable() == 1
+    return lib
+
+
+def ref_eval(lib, wx, wy, scenes, n_speeds=None, speed_offsets=None, with_frame=True, prm=None):
+    """Run the reference-compiled checker. prm (a ppamd.Params) assigns the reference's tunable
+    globals (src/main.cpp:39-49) and the horizon (libppref_n.so only; the pristine build refuses
+    any N but 50) for this call, and supplies n_speeds/speed_offsets; the defaults are restored
+    afterwards."""
+    if prm is not None:
+        n_speeds = prm.n_speeds
+        speed_offsets = [prm.speed_offsets[i] for i in range(n_speeds - 1)]
+        assert lib.ref_set_params(C.byref(prm)) == 0, "reference build cannot run these params"
+    N = prm.n_points if prm is not None else 50
     S = int(scenes["ego_x"].shape[0])
     Cn = ppamd.NUM_LANES * n_speeds
-    out = {"ref_next": np.zeros((S, 50, 2)), "ref_n": np.zeros(S, np.int32),
-           "ref_T": np.zeros(S, np.int32), "paths": np.full((S, Cn, 50, 2), np.nan),
+    out = {"ref_next": np.zeros((S, N, 2)), "ref_n": np.zeros(S, np.int32),
+           "ref_T": np.zeros(S, np.int32), "paths": np.full((S, Cn, N, 2), np.nan),
            "path_len": np.zeros((S, Cn), np.int32), "info": np.zeros((S, 8))}
     offs = np.zeros(ppamd.MAX_SPEEDS)
     offs[: len(speed_offsets)] = speed_offsets
@@ -207,10 +231,15 @@ def ref_eval(lib, wx, wy, scenes, n_speeds, speed_offsets, with_frame=True):
     wy = np.ascontiguousarray(wy, np.float64)
     ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int))
     dp = lambda a: a.ctypes.data_as(_dp)
-    with quiet_stdout():
-        rc = lib.ref_eval(dp(wx), dp(wy), len(wx), C.byref(b), n_speeds, dp(offs), int(with_frame),
-                          dp(out["ref_next"]), ip(out["ref_n"]), ip(out["ref_T"]),
-                          dp(out["paths"]), ip(out["path_len"]), dp(out["info"]))
+    try:
+        with quiet_stdout():
+            rc = lib.ref_eval(dp(wx), dp(wy), len(wx), C.byref(b), n_speeds, dp(offs), int(with_frame),
+                              dp(out["ref_next"]), ip(out["ref_n"]), ip(out["ref_T"]),
+                              dp(out["paths"]), ip(out["path_len"]), dp(out["info"]))
+    finally:
+        if prm is not None:
+            dflt = ppamd.default_params()
+            assert lib.ref_set_params(C.byref(dflt)) == 0
     assert rc == 0
     return out
 
@@ -278,9 +307,14 @@ TOL = 1e-6        # max |dxy| per point, metres
 
 
 def max_err(a, b):
-    """Largest |a - b| over finite values; the NaN pattern must be identical."""
-    fa, fb = np.isfinite(a), np.isfinite(b)
-    assert (fa == fb).all(), f"NaN pattern differs at {np.count_nonzero(fa != fb)} values"
+    """Largest |a - b| over the finite values. The NaN patterns must be identical, and infinite
+    values must be equal on both sides (same sign, same places)."""
+    na, nb = np.isnan(a), np.isnan(b)
+    assert (na == nb).all(), f"NaN pattern differs at {np.count_nonzero(na != nb)} values"
+    ia, ib = np.isinf(a), np.isinf(b)
+    assert (ia == ib).all() and (a[ia] == b[ia]).all(), \
+        f"infinite values differ at {np.count_nonzero((ia != ib) | (ia & (a != b)))} values"
+    fa = ~(na | ia)
     return float(np.abs(a[fa] - b[fa]).max()) if fa.any() else 0.0
 
 

@@ -68,3 +68,33 @@ def test_argument_validation_without_gpu():
     x = np.zeros(5)      # duplicate waypoints: Map::Init would divide by zero
     assert ppamd.lib.pp_map_create(x.ctypes.data_as(ppamd._dp), x.ctypes.data_as(ppamd._dp), 5, C.byref(h)) == -1
     assert ppamd.lib.pp_timing_read(m.handle, 99, None, None) == -1
+
+
+def test_plan_batch_host_null_inputs_rejected_without_gpu():
+    """pp_plan_batch_host gathers small batches into its pinned mirror with host memcpy, so every
+    host input pointer it would read is checked first: a NULL field (here: each field once, and
+    one table array with the table enabled) is PP_ERR_ARG before any HIP call, never a crash."""
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    prm = ppamd.default_params()
+    S = 4
+    sc = ppamd.alloc_scenes(S, 12)
+    res = ppamd.alloc_result(S, prm)
+    R = ppamd.result_struct(res)
+    fields = ["ego_x", "ego_y", "ego_yaw_deg", "ego_speed_mph", "prev_x", "prev_y", "n_prev",
+              "prev_target_lane", "n_cars", "car_id", "car_x", "car_y", "car_vx", "car_vy"]
+    for f in fields:
+        b = ppamd.scene_struct(sc)
+        setattr(b, f, None)
+        assert ppamd.lib.pp_plan_batch_host(m.handle, 0, C.byref(b), C.byref(prm), C.byref(R), None) == -1, f
+    tab = {k: np.zeros((12, S), np.int32 if k in ("tab_valid", "tab_lane") else np.float64)
+           for k in ("tab_valid", "tab_lane", "tab_s", "tab_d", "tab_vs", "tab_vd", "tab_vx", "tab_vy")}
+    for f in tab:
+        if f == "tab_valid":
+            continue
+        b = ppamd.scene_struct(sc)
+        b.tab_slots = 12
+        for k, v in tab.items():
+            setattr(b, k, v.ctypes.data)
+        setattr(b, f, None)
+        assert ppamd.lib.pp_plan_batch_host(m.handle, 0, C.byref(b), C.byref(prm), C.byref(R), None) == -1, f

@@ -205,6 +205,43 @@ class TestCarTableGPU:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("S", [37, 5000])
+def test_table_padding_with_int32_max_car_id(S):
+    """pp_cartable.h pads a scene's slots past its union with id INT32_MAX; a real car may carry
+    that id too. With an empty table and every car reported, the frame must equal the table-free
+    evaluation for every K1 group size: the padding slots repeat the last id and match no row."""
+    import torch
+    wx, wy = oracle_lib.highway_map()
+    m = ppamd.Map(wx, wy)
+    dev = torch.device("cuda", 0)
+    host = ppamd.synth_host(m, S, seed=616, first=5_000_000)
+    host["car_id"][11] = np.int32(2 ** 31 - 1)
+    prm = ppamd.default_params(emit_paths=True)
+
+    def run(d):
+        dd = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+        rr = ppamd.alloc_result(S, prm, xp="torch", device=dev)
+        ppamd.evaluate(m, dd, prm, rr, device=0)
+        torch.cuda.synchronize()
+        return ppamd.result_to_numpy(rr), {k: dd[k].cpu().numpy() for k in dd}
+
+    base, _ = run(host)
+    sc = ppamd.add_car_table(dict(host), slots=16)
+    sc["tab_id"][:12] = host["car_id"]
+    sc["tab_id"][12:] = 2 ** 31 - 1                     # padding: INT32_MAX, empty
+    try:
+        for G in (1, 2, 4, 8, 16):
+            ppamd.set_prep_group(G)
+            got, st = run(sc)
+            for k, v in base.items():
+                assert np.array_equal(np.ascontiguousarray(v).view(np.uint8),
+                                      np.ascontiguousarray(got[k]).view(np.uint8)), (G, k)
+            assert (st["tab_valid"][12:] == 0).all(), G
+    finally:
+        ppamd.set_prep_group(0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("S", [1, 37, 600, 5000])
 def test_table_mode_group_invariance(S):
     """Car-table mode through K1 with G = 1 (one lane per scene) and G = 2..16 (the grouped K1: slots

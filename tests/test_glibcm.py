@@ -32,8 +32,10 @@ def args(n, seed):
 
 
 def same(a, b):
-    return np.array_equal(a.view(np.uint64), b.view(np.uint64)) or \
-        bool(((a == b) | (np.isnan(a) & np.isnan(b))).all())
+    """Bit for bit (signed zeros included: atan2 and the standstill branch are sign sensitive);
+    NaNs match any NaN payload."""
+    a, b = np.ascontiguousarray(a, np.float64), np.ascontiguousarray(b, np.float64)
+    return bool(((a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))).all())
 
 
 def test_oracle_builds_call_sin_and_cos_separately():

@@ -1,10 +1,12 @@
-"""pp_params beyond the reference's constants (src/main.cpp:39-49 hard-codes relaxed_acc,
-maximum_acc, max_speed, car_length, safety_distance, keep_distance; include/pp.h makes them
-parameters). The reference cannot run these sets, so the oracle restatement, pinned at the
-defaults by the golden vectors, is the checker. Parity is unpinned against the reference
-itself for non-default values. On the GPU the HIP path must equal the oracle under the strict
-contract (oracle_lib.compare). k_prep's range proofs for the unchecked divisions depend on
-speeds and ramp times, so the sets move those: a lower and a higher acceleration limit, slower and
+"""pp_params beyond the reference's defaults (src/main.cpp:39-49: relaxed_acc, maximum_acc,
+max_speed, car_length, safety_distance, keep_distance, ... are mutable globals there; the horizon
+is the literal 50 at :854/:1039). Every set below is pinned to the reference's own code by
+tests/test_golden_n.py (fixtures from oracle/_ref/libppref_n.so: the globals assigned per set, the
+two point-count literals replaced by the set's horizon); only the cost extension (cost_mode,
+costs) has no reference counterpart. Here, on 3,000 fresh scenes per set, the HIP path must equal
+the restatement under the strict contract (oracle_lib.compare). k_prep's range proofs for the
+unchecked divisions depend on speeds and ramp times, so the sets move those: a lower and a higher
+acceleration limit, slower and
 faster speed caps, shorter and longer horizons, other grids, and both cost modes. Each set also
 checks that the paths-free (bench) evaluation equals the all-paths one."""
 import numpy as np
