@@ -99,13 +99,61 @@ def load_valu_peak():
         return None, None
 
 
-def load_pmc(tag):
-    """Per-launch counters of the committed rocprofv3 PMC summary (profiles/pmc_summary.json)."""
+def load_pmc_all():
+    """The committed rocprofv3 PMC summary (profiles/pmc_summary.json): per launch-shape tag."""
     p = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
-        return json.load(open(p)).get(tag)
+        return json.load(open(p))
     except Exception:
+        return {}
+
+
+def pmc_tag(S, Cn, N, emit_paths, D):
+    return f"k_cand_S{S}_C{Cn}_N{N}" + ("_paths" if emit_paths else "") + (f"_D{D}" if D > 1 else "")
+
+
+def pmc_for(pmc_all, S, Cn, N, emit_paths, D):
+    """The PMC entry of this launch shape: the exact tag, else the largest profiled launch with the
+    same candidates per scene, horizon, paths mode and draws (counter bytes and instructions per
+    candidate carry over between batch sizes of one shape). Entries must state their launch size
+    (candidates_per_launch): a counter total is meaningless without it."""
+    exact = pmc_all.get(pmc_tag(S, Cn, N, emit_paths, D))
+    cands = [exact] if exact else [
+        e for e in pmc_all.values()
+        if (e.get("candidates_per_scene"), e.get("n_points"), e.get("emit_paths"), e.get("draws", 1)) ==
+        (Cn, N, bool(emit_paths), D)]
+    if not cands:
         return None
+    e = max(cands, key=lambda e: e.get("candidates_per_launch") or 0)
+    if not e.get("candidates_per_launch"):
+        raise ValueError(f"profiles/pmc_summary.json entry without candidates_per_launch: {e.get('source')}")
+    return e
+
+
+def workload_name(S, Cn, n_speeds, N, emit_paths, D, rollout):
+    """Which BASELINE.json config a run measures (configs[1..4] = configs 2..5)."""
+    if rollout:
+        return "closed-loop rollout (SURVEY.md §8(f) row 1)"
+    if D > 1 and n_speeds == 1 and N == 50:
+        return "BASELINE config 4"
+    if emit_paths and n_speeds == 8 and N == 100:
+        return "BASELINE config 3"
+    if S == 4096 and n_speeds == 5 and N == 50 and not emit_paths and D == 1:
+        return "BASELINE config 2"
+    if n_speeds == 5 and N == 50 and not emit_paths and D == 1:
+        return "BASELINE config 5"
+    return "custom workload"
+
+
+def roofline_fields(pmc, cands_launch, bpc, k_ms):
+    """traffic (dominant kernel) and traffic_pipeline (every kernel of a step) per launch of this
+    run, from the PMC entry's bytes per candidate."""
+    if not pmc:
+        return None, None
+    pc = pmc["candidates_per_launch"]
+    traffic = pmc["hbm_bytes_per_launch"] / pc * cands_launch
+    pipe = pmc["pipeline_bytes_per_step"] / pc * cands_launch if pmc.get("pipeline_bytes_per_step") else None
+    return traffic, pipe
 
 
 def parse(argv=None):
@@ -134,6 +182,9 @@ def parse(argv=None):
                     help="skip the host-buffer (PCIe-inclusive) side measurement")
     ap.add_argument("--pcie-chunks", type=int, default=8,
                     help="chunks of the host-buffer pipeline (H2D / evaluate / D2H overlapped across chunks)")
+    ap.add_argument("--debug", action="append", default=[], metavar="KEY=VALUE",
+                    help="library debug switch for A/B runs (include/pp.h PP_DBG_*): prep_group=G, "
+                         "prep_waves=3|4, shape=1|2|3; never part of a reported bench line")
     ap.add_argument("--cpu-ranks", action="store_true",
                     help="launcher rehearsal without a GPU: every rank evaluates its shard with the CPU oracle")
     return ap.parse_args(argv)
@@ -402,6 +453,10 @@ def main(argv=None):
 
     import torch
     import ppamd
+    keys = {"prep_group": ppamd.DBG_PREP_GROUP, "prep_waves": ppamd.DBG_PREP_WAVES, "shape": ppamd.DBG_SHAPE}
+    for kv in a.debug:
+        k, _, v = kv.partition("=")
+        ppamd.debug_set(keys[k], int(v))
     # one GPU per local rank; more local ranks than GPUs share them round-robin (a rehearsal of the
     # N-rank path on a smaller box: a per-GPU timing is then not a scaling figure)
     ngpu = torch.cuda.device_count()
@@ -517,25 +572,18 @@ def main(argv=None):
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
     cands_launch = S * Cn
     achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
-    tag = f"k_cand_S{CONFIG5_SCENES if not (a.emit_paths or D > 1) else S}_C{Cn}_N{a.n_points}" + \
-        ("_paths" if a.emit_paths else "") + (f"_D{D}" if D > 1 else "")
-    pmc = load_pmc(tag)
-    traffic = traffic_pipe = None
-    if pmc:
-        # per-candidate counter bytes of the profiled launch, scaled to this launch
-        pc = pmc.get("candidates_per_launch") or (CONFIG5_SCENES * Cn)
-        traffic = pmc["hbm_bytes_per_launch"] / pc * cands_launch
-        if pmc.get("pipeline_bytes_per_step"):
-            traffic_pipe = pmc["pipeline_bytes_per_step"] / pc * cands_launch
+    pmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D)
+    traffic, traffic_pipe = roofline_fields(pmc, cands_launch, bpc, k_cand_ms)
+    wname = workload_name(S, Cn, a.n_speeds, a.n_points, a.emit_paths, D, a.rollout)
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",
         "value": value, "unit": "candidate trajectories/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
         "scaling": a.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (Philox scenes on highway_map.csv, seeded; SURVEY.md §8(d))",
-        "config": {"workload": (f"BASELINE config 4: {total_scenes} scenes x {D} sensor-noise draws x 3 lanes x "
+        "config": {"workload": (f"{wname}: {total_scenes} scenes x {D} sensor-noise draws x 3 lanes x "
                                 f"{a.n_speeds} speeds, per-scene argmin over draws" if D > 1 else
-                                f"BASELINE config 5: {total_scenes} scenes x 3 lanes x {a.n_speeds} speeds")
+                                f"{wname}: {total_scenes} scenes x 3 lanes x {a.n_speeds} speeds")
                                + (f" sharded over {world} GPUs" if a.scaling == "strong" else f" ({S} per GPU)")
                                + f", {a.n_points}-pt horizon"
                                + (", all paths emitted" if a.emit_paths else ", winner path + costs")
@@ -549,9 +597,13 @@ def main(argv=None):
         "per_rank_kernels_ms": per_rank,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_cand", "algorithmic_bytes_per_candidate": bpc,
+                     "kernel": ", ".join(pmc["kernels"]) if pmc and pmc.get("kernels") else "k_cand",
+                     "algorithmic_bytes_per_candidate": bpc,
                      "traffic_pipeline": traffic_pipe,
-                     "traffic_source": (pmc or {}).get("source")},
+                     "traffic_source": (pmc or {}).get("source"),
+                     "traffic_profiled_launch": ({k: pmc.get(k) for k in ("scenes", "candidates_per_scene", "n_points",
+                                                                           "candidates_per_launch", "kernels")}
+                                                 if pmc else None)},
     }
     if weak:
         out["weak_scaling"] = weak
@@ -561,7 +613,7 @@ def main(argv=None):
     peak, peak_add = load_valu_peak()
     if pmc and peak:
         c = pmc["counters"]
-        pc = pmc.get("candidates_per_launch") or (CONFIG5_SCENES * Cn)
+        pc = pmc["candidates_per_launch"]
         f64 = sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                            "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")) / pc * cands_launch
         allv = c.get("SQ_INSTS_VALU", 0.0) / pc * cands_launch

@@ -41,7 +41,9 @@ struct CarTable {
     }
     // writes slots [0, n_slots) of scene i: the union in ascending id order, then padding
     // (id INT32_MAX, empty) up to n_slots. Returns the union size, or -1 if it exceeds n_slots.
-    int layout(const int32_t* ids, int n, const Slots& t, int64_t i, int n_slots) const {
+    // poison (PP_DBG_POISON): the state of every slot that holds no entry is NaN / INT32_MAX
+    // instead of 0 (the kernels must write a reported car's slot before anything reads it).
+    int layout(const int32_t* ids, int n, const Slots& t, int64_t i, int n_slots, bool poison = false) const {
         std::vector<int32_t> u;
         u.reserve(cars.size() + n);
         for (const auto& kv : cars) u.push_back(kv.first);
@@ -63,8 +65,9 @@ struct CarTable {
             } else {
                 t.id[x] = INT32_MAX;
             }
-            t.valid[x] = 0; t.lane[x] = 0;
-            t.s[x] = t.d[x] = t.vs[x] = t.vd[x] = t.vx[x] = t.vy[x] = 0.0;
+            const double z = poison ? __builtin_nan("") : 0.0;
+            t.valid[x] = 0; t.lane[x] = poison ? INT32_MAX : 0;
+            t.s[x] = t.d[x] = t.vs[x] = t.vd[x] = t.vx[x] = t.vy[x] = z;
         }
         return (int)u.size();
     }

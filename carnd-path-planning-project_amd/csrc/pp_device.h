@@ -236,9 +236,6 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
     return an == 0.0 ? q0 : q;
 }
 
-#ifndef PP_MATCH_BF
-#define PP_MATCH_BF 0
-#endif
 // lane_matching on a map with fastm: the same walk, with each lane segment's rdenom and its
 // reciprocal from the tables (the division snom^2 / rdenom by div_by_rcp: the same correctly
 // rounded value), and the waypoint indices stepped instead of re-wrapped.
@@ -270,23 +267,9 @@ __device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double
             const double rn = pdx * dx + pdy * dy;
             const double snom = pdx * dy - pdy * dx;
             double rnom, dsq;
-#if PP_MATCH_BF
-            // the three cases as selects (same operations; the wave runs every case anyway when
-            // its lanes' points fall on different sides of the segment)
-            {
-                const bool lo = rn < -1, hi = !lo && rn > den;
-                const double dlo = pdx * pdx + pdy * pdy;
-                const double hx = x - bx, hy = y - by;
-                const double dhi = hx * hx + hy * hy;
-                const double din = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]);
-                rnom = lo ? 0.0 : (hi ? den : rn);
-                dsq = lo ? dlo : (hi ? dhi : din);
-            }
-#else
             if (rn < -1) { rnom = 0; dsq = pdx * pdx + pdy * pdy; }                            // :227-231
             else if (rn > den) { rnom = den; dsq = (x - bx) * (x - bx) + (y - by) * (y - by); }   // :232-236
             else { rnom = rn; dsq = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]); }
-#endif
             if (dsq < best) {
                 best = dsq;
                 improved = true;
@@ -350,9 +333,6 @@ __device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double
 // - an improvement records only its lane (and the best distance); the iteration's segment, the
 //   lane's running sum_s and ratio shift are kept once per improving iteration, and the recorded
 //   projection's rnom/snom are recomputed after the walk by the same operations.
-#ifndef PP_MATCH_CARRY      // carry the segment's end points across iterations (register pressure)
-#define PP_MATCH_CARRY 0
-#endif
 __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const double ratio[NL], double x,
                                           double y, double& out_s, double& out_d, int& out_lane,
                                           int& out_next_wp) {
@@ -364,14 +344,6 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
     double sum_s[NL], sr[NL];
 #pragma unroll
     for (int l = 0; l < NL; l++) { sum_s[l] = 0; sr[l] = ratio[l]; }
-#if PP_MATCH_CARRY
-    double ax[NL], ay[NL], bx[NL], by[NL];
-#pragma unroll
-    for (int l = 0; l < NL; l++) {
-        ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a];
-        bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b];
-    }
-#endif
     double best = 1000 * 1000;
     bool found = false;
     int b_lane = 0, k_cur = 0, k_b = 0, k_a = 0;
@@ -382,12 +354,8 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
         int il = 0;
 #pragma unroll
         for (int lane = 0; lane < NL; lane++) {
-#if PP_MATCH_CARRY
-            const double pax = ax[lane], pay = ay[lane], pbx = bx[lane], pby = by[lane];
-#else
             const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
             const double pbx = m.lc_x[lane * n + b], pby = m.lc_y[lane * n + b];
-#endif
             const double den = m.lden[lane * n + b];
             const double pdx = x - pax, dx = pbx - pax;                        // helpers.h:203-207
             const double pdy = y - pay, dy = pby - pay;
@@ -424,40 +392,14 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             cur++;
             a = b;
             b = b + 1 == n ? 0 : b + 1;
-#if PP_MATCH_CARRY
-            if (__builtin_expect(cur - 1 < -n, 0)) {
-                a = wpi(cur - 1, n); b = wpi(cur, n);
-#pragma unroll
-                for (int l = 0; l < NL; l++) { ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a]; }
-            } else {
-#pragma unroll
-                for (int l = 0; l < NL; l++) { ax[l] = bx[l]; ay[l] = by[l]; }
-            }
-#pragma unroll
-            for (int l = 0; l < NL; l++) { bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b]; }
-#else
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
-#endif
         } else {
 #pragma unroll
             for (int l = 0; l < NL; l++) { sum_s[l] -= sr[l] * m.llen[l * n + b]; sr[l] = 1; }
             cur--;
             b = a;
             a = a == 0 ? n - 1 : a - 1;
-#if PP_MATCH_CARRY
-            if (__builtin_expect(cur - 1 < -n, 0)) {
-                a = wpi(cur - 1, n); b = wpi(cur, n);
-#pragma unroll
-                for (int l = 0; l < NL; l++) { bx[l] = m.lc_x[l * n + b]; by[l] = m.lc_y[l * n + b]; }
-            } else {
-#pragma unroll
-                for (int l = 0; l < NL; l++) { bx[l] = ax[l]; by[l] = ay[l]; }
-            }
-#pragma unroll
-            for (int l = 0; l < NL; l++) { ax[l] = m.lc_x[l * n + a]; ay[l] = m.lc_y[l * n + a]; }
-#else
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
-#endif
         }
     }
     if (found) {                                                   // :214-227, last improvement

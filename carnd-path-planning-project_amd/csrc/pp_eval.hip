@@ -99,144 +99,48 @@ __device__ __forceinline__ MapV map_view(const double* b, int n, int fastm = 0) 
     return m;
 }
 
-#ifndef PP_STEP_FAST
-#define PP_STEP_FAST 1
-#endif
-#ifndef PP_WIDE_UNIT           // k_cand wide turns: atan2_unit + fmod_2pi_small (no fallbacks)
-#define PP_WIDE_UNIT 1
-#endif
-#ifndef PP_LOOP_UNROLL         // candidate loop unroll factor (loop-carried step direction copies)
-#define PP_LOOP_UNROLL 1
-#endif
-#ifndef PP_SPL_A0              // cached spline segment: extrapolation folded into the cubic form
-#define PP_SPL_A0 1
-#endif
-// PP_NT: the winner record (written once by k_cand, read once by k_emit) and next_x/next_y
-// (written once) as nontemporal (streaming) accesses
-#ifndef PP_NT
-#define PP_NT 1
-#endif
-#if PP_NT
+// The winner record (written once by k_cand, read once by k_emit), next_x/next_y (written once)
+// and every emitted path point are nontemporal (streaming) accesses
 #define PP_ST(p, v) __builtin_nontemporal_store((v), (p))
 #define PP_LD(p) __builtin_nontemporal_load(p)
-#else
-#define PP_ST(p, v) (*(p) = (v))
-#define PP_LD(p) (*(p))
-#endif
-#ifndef PP_PATHS_NT            // emit_paths: every path point as a nontemporal (streaming) store
-#define PP_PATHS_NT 1
-#endif
 // one (x, y) path point: a 16-B store (p 16-B aligned: paths are [.., c] pairs of doubles)
 __device__ __forceinline__ void st_xy(double* p, double x, double y) {
     typedef double dv2 __attribute__((ext_vector_type(2)));
     const dv2 xy = {x, y};
-    if (PP_PATHS_NT) __builtin_nontemporal_store(xy, (dv2*)p);
-    else *(dv2*)p = xy;
+    __builtin_nontemporal_store(xy, (dv2*)p);
 }
-#ifndef PP_EMIT_CHUNK          // k_emit: recorded steps loaded together per lane
-#define PP_EMIT_CHUNK 4
-#endif
-// Winner record layout (k_cand -> k_emit); room = N - K steps of scene s, rstride = room S.
-//   0 (product): point-major arrays, pos_x at rec[g S + s], pos_y at rec[rstride + g S + s], the
-//     rotation of an adjusted step at rec[2 rstride + g S + s] (every address of scene s is = s mod S);
-//   1 (PP_REC_PAIR=1, measured slower): one 16-B (pos_x, pos_y) pair at rec[2 (g S + s)], the
-//     rotations behind the pairs of the longest walk, rec[2 N S + g S + s];
-//   2 (PP_REC_PAIR=2): wave-blocked, the 64 scenes of a wave own one contiguous 3 N x 64 block:
-//     pos_x at rec[B + g 64 + l], pos_y at rec[B + (N + g) 64 + l], rotation at rec[B + (2N + g) 64
-//     + l], B = (s / 64) 3 N 64, l = s mod 64 (a wave's record is 3 N 512 contiguous bytes instead
-//     of 3 N rows S 8 bytes apart; the buffer's scene capacity is a multiple of 64).
-#ifndef PP_REC_PAIR
-#define PP_REC_PAIR 0
-#endif
-typedef double pp_dv2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ int64_t rec_wb(int N, int64_t s) { return (s >> 6) * (3 * (int64_t)N * 64) + (s & 63); }
-__device__ __forceinline__ double* rec_px(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
-    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + g * 64 : PP_REC_PAIR == 1 ? rec + 2 * (g * S + s) : rec + g * S + s;
+// Tuning constants (each measured against its alternatives):
+constexpr int kEmitChunk = 4;      // k_emit: recorded steps loaded together per lane (large batches)
+constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
+constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
+constexpr int kCandWaves = 4;      // k_cand waves per SIMD (<= 128 VGPRs)
+// Winner record (k_cand -> k_emit), room = N - K steps of scene s, rstride = room S: point-major
+// arrays, pos_x at rec[g S + s], pos_y at rec[rstride + g S + s], the rotation of an adjusted step
+// at rec[2 rstride + g S + s] (every address of scene s is = s mod S: a wave's accesses coalesce)
+__device__ __forceinline__ double* rec_px(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s) {
+    (void)rstride;
+    return rec + g * S + s;
 }
-__device__ __forceinline__ double* rec_py(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
-    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + ((int64_t)N + g) * 64
-         : PP_REC_PAIR == 1 ? rec + 2 * (g * S + s) + 1 : rec + rstride + g * S + s;
+__device__ __forceinline__ double* rec_py(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s) {
+    return rec + rstride + g * S + s;
 }
-__device__ __forceinline__ double* rec_rot(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
-    return PP_REC_PAIR == 2 ? rec + rec_wb(N, s) + (2 * (int64_t)N + g) * 64
-         : PP_REC_PAIR == 1 ? rec + 2 * (int64_t)N * S + g * S + s : rec + 2 * rstride + g * S + s;
+__device__ __forceinline__ double* rec_rot(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s) {
+    return rec + 2 * rstride + g * S + s;
 }
-__device__ __forceinline__ const double* rec_rot(const double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s) {
-    return rec_rot((double*)rec, rstride, N, g, S, s);
+__device__ __forceinline__ const double* rec_rot(const double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s) {
+    return rec_rot((double*)rec, rstride, g, S, s);
 }
-__device__ __forceinline__ void rec_st(double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s,
+__device__ __forceinline__ void rec_st(double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
                                        double x, double y) {
-    if (PP_REC_PAIR == 1) {
-        const pp_dv2 xy = {x, y};
-        pp_dv2* p = (pp_dv2*)rec_px(rec, rstride, N, g, S, s);
-        if (PP_NT) __builtin_nontemporal_store(xy, p); else *p = xy;
-    } else {
-        PP_ST(rec_px(rec, rstride, N, g, S, s), x);
-        PP_ST(rec_py(rec, rstride, N, g, S, s), y);
-    }
+    PP_ST(rec_px(rec, rstride, g, S, s), x);
+    PP_ST(rec_py(rec, rstride, g, S, s), y);
 }
-__device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int N, int64_t g, int64_t S, int64_t s,
+__device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int64_t g, int64_t S, int64_t s,
                                        double& x, double& y) {
     double* r = (double*)rec;
-    if (PP_REC_PAIR == 1) {
-        const pp_dv2* p = (const pp_dv2*)rec_px(r, rstride, N, g, S, s);
-        const pp_dv2 xy = PP_NT ? __builtin_nontemporal_load(p) : *p;
-        x = xy.x; y = xy.y;
-    } else {
-        x = PP_LD(rec_px(r, rstride, N, g, S, s));
-        y = PP_LD(rec_py(r, rstride, N, g, S, s));
-    }
+    x = PP_LD(rec_px(r, rstride, g, S, s));
+    y = PP_LD(rec_py(r, rstride, g, S, s));
 }
-#ifndef PP_EMIT_ROTATE
-#define PP_EMIT_ROTATE 1
-#endif
-#ifndef PP_TEAM_SETUP
-#define PP_TEAM_SETUP 1
-#endif
-#ifndef PP_WIN_INLINE          // reference mode: winner lanes write next_x/next_y in k_cand (no k_emit)
-#define PP_WIN_INLINE 0
-#endif
-#ifndef PP_SEG_MODE
-#define PP_SEG_MODE 3
-#endif
-// segments of the control-point walk loaded ahead (get_lane_pos_fwd)
-#ifndef PP_WALK_PF
-#define PP_WALK_PF 4
-#endif
-// k_prep visits the cars nearest first (ties by iteration index keep the reference's results)
-#ifndef PP_CAR_SORT
-#define PP_CAR_SORT 1
-#endif
-#ifndef PP_CAR_SORT_BATCH
-#define PP_CAR_SORT_BATCH 0
-#endif
-// standing candidates (speed 0) take the turn series whatever the angle
-#ifndef PP_ROT_IDENT            // output-frame turns by Taylor + angle difference (run_candidate; measured slower)
-#define PP_ROT_IDENT 0
-#endif
-#ifndef PP_STAND_SERIES
-#define PP_STAND_SERIES 0
-#endif
-// phase A's serial steps (control-point distance rule, band sweeps) on the block's first wave
-#ifndef PP_SERIAL_WAVE
-#define PP_SERIAL_WAVE 1
-#endif
-#ifndef PP_ANGLE_CROSS
-#define PP_ANGLE_CROSS 1
-#endif
-// Divisions of the candidate loop as a reciprocal and one correction step (ppm::div_rcp):
-// bit 0: the two divisions by the step length d, bit 1: speed / 50, bit 2: the speed ramp / ttime
-// (bit 2: k_cand<false> divides the ramp unchecked; k_cand<true> keeps the checked form)
-#ifndef PP_DIV_RCP
-#define PP_DIV_RCP 7
-#endif
-// the override's divisions (na / 50 and SpeedController::override_speed) by reciprocals
-#ifndef PP_OVR_RCP
-#define PP_OVR_RCP 1
-#endif
-#ifndef PP_PREP_WAVES
-#define PP_PREP_WAVES 3
-#endif
 // kLdsMap: the map (kMapArrays n doubles) is staged in LDS (n <= kLdsMapMax: <= 62.4 KB, 600
 // waypoints at three lanes); larger maps are read from global memory (L2-resident) by the same code.
 constexpr int kLdsMapMax = 62400 / (8 * kMapArrays);
@@ -591,95 +495,10 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
     cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
 }
 
-// K1's car pass without a car table and without Monte-Carlo draws: lane_matching in two passes
-// (pp_device.h, walk_finish). Pass 1 runs all of a lane's car walks as one flat loop — a lane whose
-// walk ends takes its next car in the same iteration — so the lanes of a wave stay busy until their
-// own total walk length is spent, instead of idling at every car until the wave's longest walk for
-// that car ends. Each walk's outcome is a 16-bit word in LDS (kFlatCars cars per round). Pass 2
-// visits the cars in row order (the reference's own order, src/main.cpp:1325-1411; coalesced
-// reads), rebuilds each projection from its word and feeds the planner.
-// Measured and kept opt-in (PP_PREP_FLAT=1; bit-identical, the GPU suite passes with it): at 3
-// waves/SIMD k_prep 2.07 -> 2.23 ms on the config-5 batch. A lane that finishes a walk loads its
-// next car's position while the others walk on; the wave's next read of that register waits for
-// the most recent of those loads, so nearly every iteration pays a memory latency.
-#ifndef PP_PREP_FLAT
-#define PP_PREP_FLAT 0
-#endif
-constexpr int kFlatCars = 16;
-constexpr size_t kFlatLds = sizeof(uint16_t) * kFlatCars * 256;   // per 256-lane block
-constexpr size_t kPrepLdsFlat = PP_PREP_FLAT ? kFlatLds : 0;       // k_prep's dynamic LDS after the map
-
-__device__ __forceinline__ void prep_cars_flat(const MapV& m, const pp_scene_batch& in, const pp_params& P,
-                                               int64_t S, int64_t s, const EgoSt& e, int T_in, int iters,
-                                               uint16_t* res, PlanAcc& acc, uint32_t& status) {
-    const int n = m.n;
-    const int wmax = 4 * n + 8;                       // lane_matching's bound (never reached)
-    const int a0 = wpi(e.ref_wp - 1, n), b0 = wpi(e.ref_wp, n);
-    for (int c0 = 0; c0 < iters; c0 += kFlatCars) {
-        const int c1 = iters - c0 < kFlatCars ? iters : c0 + kFlatCars;
-        // pass 1: the walks of cars [c0, c1), the next car's position loaded one walk ahead
-        int j = c0;
-        double x = in.car_x[(int64_t)j * S + s], y = in.car_y[(int64_t)j * S + s];
-        double nx = 0, ny = 0;
-        if (j + 1 < c1) { nx = in.car_x[(int64_t)(j + 1) * S + s]; ny = in.car_y[(int64_t)(j + 1) * S + s]; }
-        int cur = e.ref_wp, a = a0, b = b0, dir = 0, itc = 0, kc = 0, kl = 0;
-        bool found = false;
-        double best = 1000 * 1000;
-        for (;;) {
-            PP_DIAGC(16, true);
-            bool improved = false, stop = false;
-            int il = 0;
-#pragma unroll
-            for (int l = 0; l < NL; l++) {                           // src/main.cpp:215-252
-                double rnom, snom, den;
-                const double dsq = seg_dsq(m, l, a, b, x, y, rnom, snom, den);
-                if (dsq < best) { best = dsq; improved = true; il = l; }
-                if (rnom == 0) { if (dir == 1) stop = true; dir = -1; }
-                else if (rnom == den) { if (dir == -1) stop = true; dir = 1; }
-                else stop = true;
-            }
-            if (improved) { found = true; kc = cur; kl = il; }
-            if (improved && !stop && ++itc < wmax) {                 // :253-272
-                if (dir > 0) { cur++; a = b; b = b + 1 == n ? 0 : b + 1; }
-                else { cur--; b = a; a = a == 0 ? n - 1 : a - 1; }
-                if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
-                continue;
-            }
-            uint16_t w = 0;
-            if (found) {
-                const int off = kc - e.ref_wp;
-                w = off >= -2048 && off <= 2047 ? (uint16_t)(0x8000 | (kl << 12) | (off + 2048)) : kWalkRedo;
-            }
-            res[(j - c0) * 256] = w;
-            if (++j >= c1) break;
-            x = nx; y = ny;
-            if (j + 1 < c1) { nx = in.car_x[(int64_t)(j + 1) * S + s]; ny = in.car_y[(int64_t)(j + 1) * S + s]; }
-            cur = e.ref_wp; a = a0; b = b0; dir = 0; itc = 0; found = false; best = 1000 * 1000;
-        }
-        // pass 2: row order; the projection each walk recorded, then project_speed and the planner
-        for (int r = c0; r < c1; r++) {
-            const int64_t ix = (int64_t)r * S + s;
-            const uint32_t w = res[(r - c0) * 256];
-            const double cx = in.car_x[ix], cy = in.car_y[ix];
-            double cs, cd;
-            int clane = 0, nwp = 0;
-            if (w & 0x8000) {
-                walk_finish(m, e.ref_wp, e.ratio, cx, cy, w, cs, cd, clane, nwp);
-            } else if (w != kWalkRedo || !lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
-                status |= PP_ST_CAR_UNMATCHED;                       // :1336-1341
-                continue;
-            }
-            double cvs, cvd;
-            project_speed(m, in.car_vx[ix], in.car_vy[ix], nwp, cvs, cvd);
-            acc.add(P, e, T_in, r, in.car_id[ix], cs, cd, clane, cvs, cvd);
-        }
-    }
-}
-
 // kW4: the 4-waves-per-SIMD instantiation (<= 128 VGPRs): for batches whose wave count fills
 // whole rounds of 4 waves per SIMD better than of 3 (prep_w4 in pp_eval)
 template <bool kLdsMap, bool kW4 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : PP_PREP_WAVES))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : kPrepWaves))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb,
                                               int64_t v0, int64_t v1) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
@@ -713,19 +532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
     // either reported this frame (re-matched; slot overwritten, or erased when matching fails,
     // src/main.cpp:1329-1348) or taken from its stale slot.
     const bool tab = in.tab_valid != nullptr;
-#ifdef PP_ABL_PREP_NOCARS   // diagnostic timing build: ego only
-    const int iters = 0;
-#else
     const int iters = tab ? in.tab_slots : ncar;
-#endif
-#if PP_PREP_FLAT
-    if (!tab && D == 1 && m.fastm) {      // (block-uniform) the flattened two-pass car loop
-        uint16_t* res = (uint16_t*)(smap + (kLdsMap ? kMapArrays * n : 0)) + threadIdx.x;
-        prep_cars_flat(m, in, P, S, s, e, T_in, iters, res, a, status);
-        prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
-        return;
-    }
-#endif
     // Visiting order (PlanAcc: any order once ties compare the iteration index). Without a car
     // table the rows are visited nearest first (squared distance to the ego, a 4-bit row index in
     // the low mantissa bits of a float key, sorted by a Batcher network): the k-th visit of every
@@ -734,7 +541,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
     // sentinel), the identity order is kept. (more than 16 rows: the identity order)
     uint64_t order = 0xFEDCBA9876543210ull;
     bool sorted = false;
-#if PP_CAR_SORT
     if (!tab && iters > 1 && iters <= 16) {
         uint32_t key[16];
         bool neg = false;
@@ -745,13 +551,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
                 const int64_t ix = (int64_t)j * S + s;
                 const double dx = in.car_x[ix] - e.ego_x, dy = in.car_y[ix] - e.ego_y;
                 const float f = (float)(dx * dx + dy * dy);
-#if PP_CAR_SORT_BATCH
-                // rows in batches of PP_CAR_SORT_BATCH, nearest first inside a batch: the rows a
-                // wave gathers from stay few while a batch is visited (L2 locality)
-                key[j] = ((uint32_t)(j / PP_CAR_SORT_BATCH) << 28) | ((__float_as_uint(f) >> 3) & 0x0FFFFFF0u) | (uint32_t)j;
-#else
                 key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
-#endif
                 neg |= in.car_id[ix] < 0;
             }
         }
@@ -775,7 +575,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
             sorted = true;
         }
     }
-#endif
     static_assert((2 * NL + 1) * 6 <= 64 && PP_MAX_CARS <= 64, "iteration index fields");
     int p = 0;                              // next unread row (table mode)
     for (int kk = 0; kk < iters; kk++) {
@@ -797,16 +596,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
             cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
             if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
             int nwp = 0;
-#ifdef PP_ABL_SKIP_FAR   // diagnostic timing build: cars beyond PP_ABL_SKIP_FAR metres skipped
-            if ((cx - e.ego_x) * (cx - e.ego_x) + (cy - e.ego_y) * (cy - e.ego_y) > PP_ABL_SKIP_FAR * PP_ABL_SKIP_FAR) continue;
-#endif
             PP_DIAGC(17, true);
-#ifdef PP_ABL_NO_MATCH     // diagnostic timing build: no lane matching of the cars
-            cs = e.ego_s + (cx - e.ego_x); cd = 6.0 + 0.1 * (cy - e.ego_y); clane = 1; nwp = e.ref_wp;
-            if (false) {
-#else
             if (!lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
-#endif
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;
                 continue;
@@ -826,111 +617,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : P
         a.add(P, e, T_in, it, id, cs, cd, clane, cvs, cvd);
     }
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
-}
-
-// K1 with the cars staged in LDS (large batches, no car table, <= kStRows rows, map in LDS): every
-// car field is read once, coalesced, in row order. Pass 1 visits the cars nearest first (the
-// divergence argument of k_prep) but reads their x, y from LDS, and leaves each car's Frenet
-// (s, d) in place of its x, y with (matched, lane, next waypoint) beside it; pass 2 reads id, vx,
-// vy in row order (the reference's own iteration order, src/main.cpp:1325-1411), projects the
-// velocity and feeds the planner. 512-lane blocks, 2 waves per SIMD: one map copy per CU beside
-// 12 x 512 staged (x, y) pairs (PP_PREP_ST).
-constexpr int kStRows = 12;
-constexpr int kStBlock = 512;
-template <int kUnused>
-__global__ __launch_bounds__(kStBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_prep_st(
-        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_scene_info* info, uint32_t* out_status,
-        GroupBits gb) {
-    extern __shared__ __attribute__((aligned(16))) double smap[];
-    const int n = mg.n;
-    for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
-    double2* sxy = (double2*)(smap + ((kMapArrays * n + 1) & ~1));       // [row][lane]
-    int32_t* smeta = (int32_t*)(sxy + kStRows * kStBlock);                // [row][lane]
-    __syncthreads();
-    const MapV m = map_view(smap, n, mg.fastm);
-    const int64_t S = in.n_scenes;
-    const int D = P.n_draws > 1 ? P.n_draws : 1;
-    const int64_t Sv = S * D;
-    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= Sv) return;
-    const int64_t s = D == 1 ? v : v / D;
-    const int draw = (int)(v - s * D);
-    const int tid = threadIdx.x;
-
-    EgoSt e;
-    prep_ego<1>(m, in, P, S, s, 0, e);
-    uint32_t status = e.status;
-    const int T_in = in.prev_target_lane[s];
-    int ncar = in.n_cars[s];
-    if (ncar > in.car_stride) ncar = in.car_stride;
-    // stage x, y (row order, coalesced) and the nearest-first keys (k_prep's)
-    uint32_t key[16];
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        key[j] = 0xFFFFFFF0u | (uint32_t)j;
-        if (j < kStRows && j < ncar) {
-            const int64_t ix = (int64_t)j * S + s;
-            double cx = in.car_x[ix], cy = in.car_y[ix];
-            if (draw > 0) {
-                const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
-                cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 0);
-                cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 1);
-            }
-            sxy[j * kStBlock + tid] = make_double2(cx, cy);
-            const double dx = cx - e.ego_x, dy = cy - e.ego_y;
-            const float f = (float)(dx * dx + dy * dy);
-            key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
-        }
-    }
-#pragma unroll
-    for (int pw = 1; pw < 16; pw <<= 1)
-#pragma unroll
-        for (int k = pw; k >= 1; k >>= 1)
-#pragma unroll
-            for (int j = k % pw; j < 16 - k; j += 2 * k)
-#pragma unroll
-                for (int i = 0; i < k; i++)
-                    if ((i + j) / (2 * pw) == (i + j + k) / (2 * pw)) {
-                        const uint32_t lo = key[i + j] < key[i + j + k] ? key[i + j] : key[i + j + k];
-                        const uint32_t hi = key[i + j] < key[i + j + k] ? key[i + j + k] : key[i + j];
-                        key[i + j] = lo; key[i + j + k] = hi;
-                    }
-    uint64_t order = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
-    // pass 1: Frenet matching, nearest first, from LDS
-    for (int kk = 0; kk < ncar; kk++) {
-        const int it = (int)((order >> (4 * kk)) & 15);
-        const double2 xy = sxy[it * kStBlock + tid];
-        double cs, cd;
-        int clane = 0, nwp = 0;
-        int32_t meta = 0;        // matched | lane << 1 | next waypoint * 16 (may be negative)
-        if (lane_match(m, e.ref_wp, e.ratio, xy.x, xy.y, cs, cd, clane, nwp)) {
-            sxy[it * kStBlock + tid] = make_double2(cs, cd);
-            meta = 1 | (clane << 1) | (int32_t)((uint32_t)nwp << 4);
-        }
-        smeta[it * kStBlock + tid] = meta;
-    }
-    // pass 2: row order (the reference's), velocity projection and the planner
-    PlanAcc a;
-    a.init();
-    for (int j = 0; j < ncar; j++) {
-        const int64_t ix = (int64_t)j * S + s;
-        const int id = in.car_id[ix];
-        double cvx = in.car_vx[ix], cvy = in.car_vy[ix];
-        const int32_t meta = smeta[j * kStBlock + tid];
-        if (!(meta & 1)) { status |= PP_ST_CAR_UNMATCHED; continue; }
-        if (draw > 0) {
-            const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
-            cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 2);
-            cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, j, 3);
-        }
-        const double2 sd = sxy[j * kStBlock + tid];
-        double cvs, cvd;
-        project_speed(m, cvx, cvy, meta >> 4, cvs, cvd);       // arithmetic shift: nwp
-        a.add(P, e, T_in, j, id, sd.x, sd.y, (meta >> 1) & 7, cvs, cvd);
-    }
-    prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, false, 0, T_in, e, a, status);
 }
 
 // K1 for small batches: a group of G lanes per evaluation (G = 2 ... 16; kernels k_prep_g2 ... k_prep_g16), so that a batch of a few
@@ -1083,19 +769,10 @@ struct Slot {
 // sm[(j * kKP + i) * 5 + field] — one address register per slot and immediate offsets for the five
 // fields (the field-major layout needs five: in emit_paths mode they spill, and every reload waits
 // for the lane's outstanding path stores). Otherwise field-major, sX[j * kKP + i] etc.
-#ifndef PP_SLOT_AOS
-#define PP_SLOT_AOS 1
-#endif
 __device__ __forceinline__ Slot lds_slot(double* sX, int nslot, int* sMeta, int j) {
-#if PP_SLOT_AOS
     (void)nslot;
     double* b = sX + (int64_t)j * kKP * 5;
     return Slot{b, b + 1, b + 2, b + 3, b + 4, sMeta + 4 * j, 5, 1};
-#else
-    const int64_t f = (int64_t)nslot * kKP;
-    double* b = sX + (int64_t)j * kKP;
-    return Slot{b, b + f, b + 2 * f, b + 3 * f, b + 4 * f, sMeta + 4 * j, 1, 1};
-#endif
 }
 constexpr int kMetaFallback = 1, kMetaTrunc = 2, kMetaWalkFail = 4;
 
@@ -1294,12 +971,8 @@ __device__ void team_a1(const MapV& m, const pp_scene_batch& in, const LaneGeom&
         for (int i = 1; i <= k; i++) cps = cps + g.min_cpd;
         double px, py;
         bool ok;
-#if defined(PP_ABL_A) && (PP_ABL_A & 1)   // diagnostic timing build: no map walk
-        px = g.pos_x + cps; py = g.pos_y + 0.01 * cps * cps; ok = true; (void)m;
-#else
-        if (cps > 0) get_lane_pos_fwd<PP_WALK_PF>(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
+        if (cps > 0) get_lane_pos_fwd<kWalkPf>(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
         else get_lane_pos(m, g.ref_wp, g.ratio, cps, L, px, py, ok);
-#endif
         const int j = g.npk + 1 + k;
         sl.a(j) = px; sl.b(j) = py; sl.c(j) = ok ? 1.0 : 0.0;
         const double tx0 = px - g.pos_x, ty0 = py - g.pos_y;
@@ -1413,22 +1086,21 @@ struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj
 // Output modes. The curvature adjustment (src/main.cpp:972-1018) rotates only the local->global
 // transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that the cost reads
 // never depends on it, so a cost-only lane skips the transform, its sin/cos and the stores.
-//   kOutMode 0: cost only;  2: every lane produces points;  1: lanes with out_on produce points;
-//   3: lanes with out_on RECORD their local path (pos after each step, rotation angle of each
+//   kOutMode 0: cost only;  2: every lane produces points;  3: lanes with out_on RECORD their local path (pos after each step, rotation angle of each
 //   curvature adjustment + a bitmask of the adjusted steps) for k_emit, which replays the
 //   transform — the expensive sin/cos of the adjustments leaves the candidate loop entirely.
 // Point g goes to wx[g*ws], wy[g*ws] (if wx) and px[g*ps], px[g*ps+1] (if px); in mode 3 the record
 // goes to rec[g*ws] (pos_x), rec[(RN + g)*ws] (pos_y), rec[(2 RN + g)*ws] (rotation), RN = room.
-// kCache: keep the current spline segment (bounds + coefficients) in registers; the segment
-// changes every ~10-40 steps, so most steps read no slot memory.
-template <bool kLarge, int kOutMode, bool kCache>
+// The current spline segment (bounds + coefficients) stays in registers; the segment changes every
+// ~10-40 steps, so most steps read no slot memory.
+template <bool kLarge, int kOutMode>
 __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, double cy,
                                  double angle, double ca0, double sa0, SC sc, int room, double* wx,
                                  double* wy, int64_t ws, double* px, int64_t ps, bool out_on = true,
                                  double* rec = nullptr, int dcls = 0, int64_t rs = 0) {
     (void)dcls;   // PP_DIAG builds: candidate class (|L - ego lane|) for the census
     // kOutMode 3: rec = the record base + rs (the scene), ws = the batch's scene count (rec_st)
-    const bool kOut = kOutMode == 2 || (kOutMode == 1 && out_on);
+    const bool kOut = kOutMode == 2;
     const bool kRec = kOutMode == 3 && out_on;
     const int64_t rstride = (int64_t)room * ws;
     CandRes R;
@@ -1472,7 +1144,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
                 if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, tx + cx, ty + cy);
             }
-            if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, P.n_points, ng, ws, rs, pos_x, pos_y);
+            if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
             ng++;
             R.travelled += dstep;
         }
@@ -1480,60 +1152,23 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         return R;
     }
     // cached segment: valid while seg_lo < x <= seg_hi (NaN x never valid)
-#if PP_SEG_MODE == 3
     int cnt = -1;                    // #knots with X < x (std::lower_bound position); -1: none yet
     double seg_lo = 1.0, seg_hi = -__builtin_inf(), sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
-#else
-    int cnt = 0;                     // #knots with X < x (std::lower_bound position)
-    double seg_lo = 1.0, seg_hi = 0.0, sx = 0, sa_ = 0, sb = 0, sc_ = 0, sy = 0;
-#endif
     double arg = 0, prev_speed = sc.start;
-#if PP_ANGLE_CROSS
     double uxp = 1.0, uyp = 0.0;     // previous step direction (angle 0: the local frame's x axis)
-#else
-    double prev_angle = 0;
-#endif
-#if PP_OVR_RCP
     // 1 / (target - start) for SpeedController::override_speed (constant over the walk)
     const double rds = ppm::rcp_nr(sc.target - sc.start);
-#endif
-#if PP_DIV_RCP & 4
     double rtt = ppm::rcp_nr(sc.ttime);
-#define PP_SC_SPEED(t) sc_get_speed_r<kLarge>(sc, t, rtt)
-#else
-#define PP_SC_SPEED(t) sc_get_speed(sc, t)
-#endif
-#if PP_DIV_RCP & 2
+    // the divisions by 50 and by the ramp time: reciprocal + correction (k_cand<false>: unchecked)
 #define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div50_nc(v))
-#else
-#define PP_DIV50(v) ((v) / 50)
-#endif
-#if PP_LOOP_UNROLL > 1
-#pragma unroll PP_LOOP_UNROLL
-#endif
     while (arg < 50 && ng < room) {
         PP_DIAGC(0, true);
         PP_DIAGC(2, !(s_max(cur_t - sc.shift, 0.0) > sc.ttime));
-        double speed = PP_SC_SPEED(cur_t);
+        double speed = sc_get_speed_r<kLarge>(sc, cur_t, rtt);
         double dstep = PP_DIV50(speed);
         const double x = arg + dstep;
         // tk::spline::operator() (spline.h:375-396)
-#if PP_SEG_MODE == 2
-        // no cache: x never decreases along the walk (sp_step >= 0), so the lower_bound position
-        // only moves forward; the segment's coefficients are re-read from LDS every step
-        (void)seg_lo; (void)seg_hi;
-        while (cnt < nk && sl.x(cnt) < x) cnt++;
-        {
-            const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
-            sx = sl.x(idx); sa_ = sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
-        }
-#else
-        if (!kCache || !(seg_lo < x && x <= seg_hi)
-#if PP_SEG_MODE == 9      // diagnostic timing build: the first step's segment for the whole walk
-            && ng == 0
-#endif
-        ) {
-#if PP_SEG_MODE == 3
+        if (!(seg_lo < x && x <= seg_hi)) {
             // forward miss (x passed the cached segment's end; the first step starts from cnt = -1,
             // seg_hi = -inf): x(cnt) = seg_hi < x is known, so the walk resumes one knot further
             // and the bounds come from the walk's own reads — one LDS round trip for the knot and
@@ -1551,7 +1186,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 seg_hi = xhi;
                 const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
                 sx = cnt > 0 ? xlo : xhi;
-                sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+                sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
             } else {
                 if (cnt < 0) cnt = 0;
                 while (cnt < nk && sl.x(cnt) < x) cnt++;
@@ -1559,54 +1194,24 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
                 seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
                 seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
-                sx = sl.x(idx); sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+                sx = sl.x(idx); sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
             }
-#elif PP_SEG_MODE == 1    // forward only unless x fell below the cached segment
-            if (__builtin_expect(x <= seg_lo, 0)) while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
-            else while (cnt < nk && sl.x(cnt) < x) cnt++;
-#else
-            while (cnt < nk && sl.x(cnt) < x) cnt++;
-            while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
-#endif
             PP_DIAGC(1, true);
-#if PP_SEG_MODE != 3
-            const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
-            seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
-            seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
-            sx = sl.x(idx); sa_ = (PP_SPL_A0 && cnt == 0) ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
-#endif
         }
-#endif
         const double h = x - sx;
-        double y;
-#if PP_SPL_A0
-        // kCache segments: the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0
-        // (0 h + b = b, and at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the
-        // last knot, whose a is 0 (spline.h:367): one polynomial form for every step
-        if (kCache && PP_SEG_MODE != 2) y = ((sa_ * h + sb) * h + sc_) * h + sy;
-        else
-#endif
-        if (cnt == 0 && x < sx) y = (sb * h + sc_) * h + sy;                       // left
-        else if (cnt == nk && x > sx) y = (sb * h + sc_) * h + sy;                 // right
-        else y = ((sa_ * h + sb) * h + sc_) * h + sy;
-#if PP_STEP_FAST
+        // the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0 (0 h + b = b, and
+        // at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the last knot, whose a is
+        // 0 (spline.h:367): one polynomial form for every step
+        const double y = ((sa_ * h + sb) * h + sc_) * h + sy;
         double d, rd;
         const bool dok = ppm::sqrt_rd((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y), d, rd);
-#else
-        const double d = sqrt((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y));
-#endif
         double acc = fabs(speed - prev_speed) * 50;
-#if PP_ANGLE_CROSS
         // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
         // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
         double ux, uy;
-#if !PP_STEP_FAST
-        const double rd = ppm::rcp_nr(d);
-#endif
         {
             const double ddx = x - pos_x, ddy = y - pos_y;
             ux = ddx * rd; uy = ddy * rd;
-#if PP_STEP_FAST
             if (__builtin_expect(!dok, 0)) {        // d == 0 implies !dok (q = 0 < 2^-900)
                 if (d == 0) { ux = 1.0; uy = 0.0; }
                 // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only
@@ -1620,77 +1225,34 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     ux = a / n; uy = b / n;
                 }
             }
-#else
-            if (__builtin_expect(d == 0, 0)) { ux = 1.0; uy = 0.0; }
-#endif
         }
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
-#if PP_ROT_IDENT
-        const double cr_st = cr, dt_st = dt;     // the turn's sine and cosine (curvature adjustment)
-#endif
-#if PP_STEP_FAST
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
         double adiff;
         PP_DIAGC(3, !((dt > 0 && fabs(cr) <= ppm::kStepSinMax) || speed == 0));
         PP_DIAGC(8, ng == 0 && !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
         PP_DIAGC(9, !(dt > 0));
-#ifdef PP_ABL_NO_WIDE      // diagnostic timing build: every turn through the series
-        if (true)
-#else
-        // a standing candidate (speed 0) turns by anything without consequence: its
-        // cacc = 0 * 50 * |adiff| is 0 for every finite adiff (and a curvature adjustment
-        // divides 0 by 0), so it takes the series whatever the angle (|cr| <= 1: finite)
-        if (__builtin_expect((dt > 0 && fabs(cr) <= ppm::kStepSinMax) || (PP_STAND_SERIES && speed == 0), 1))
-#endif
+        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1))
             adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
         else
-#if PP_WIDE_UNIT
             // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
             adiff = ppm::fmod_2pi_small(ppm::atan2_unit(cr, dt) + 3 * kPi) - kPi;
-#else
-            adiff = ppm::fmod_2pi(ppm::atan2_fast(cr, dt) + 3 * kPi) - kPi;
-#endif
-#else
-        double adt;
-        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1)) adt = ppm::asin_small(cr);
-        else adt = ppm::atan2_fast(cr, dt);
-        const double adiff = ppm::fmod_2pi(adt + 3 * kPi) - kPi;
-#endif
-#else
-        const double astep = ppm::atan2_fast(y - pos_y, x - pos_x);
-        const double adiff = ppm::fmod_2pi(astep - prev_angle + 3 * kPi) - kPi;
-#endif
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
         PP_DIAGC(4, acc + cacc > P.maximum_acc);
         PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
         PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
         PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
-#ifdef PP_ABL_NO_LIMITER   // diagnostic timing build: the limiter branch never runs
-        if (false) {
-#else
         if (acc + cacc > P.maximum_acc) {
-#endif
-#ifdef PP_ABL_NO_OVERRIDE  // diagnostic timing build: the speed override never runs
-            if (false) {
-#else
             if (speed > prev_speed) {                                   // :945-971
-#endif
                 double na = P.maximum_acc - cacc;
                 if (na < 0) na = 0;
-#if PP_OVR_RCP
                 const double ns = prev_speed + PP_DIV50(na);
                 sc_override_r<kLarge>(sc, cur_t, ns, rds);
-#else
-                const double ns = prev_speed + na / 50;
-                sc_override(sc, cur_t, ns);
-#endif
                 speed = ns;
                 sc.ttime += 0.02;
-#if PP_DIV_RCP & 4
                 rtt = ppm::rcp_nr(sc.ttime);
-#endif
                 dstep = PP_DIV50(speed);
                 acc = na;
                 R.flags |= PP_ST_ACC_OVERRIDE;
@@ -1714,29 +1276,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     tpy = tpy + cy;
                     const double vx = cx - tpx, vy = cy - tpy;
                     double cr, sr;
-#ifdef PP_ABL_CAND_TRIG     // diagnostic timing build (wrong results): first-order sin/cos of the turn
-                    sr = rot; cr = 1.0;
-#else
-#if PP_ROT_IDENT && PP_ANGLE_CROSS && PP_STEP_FAST
-                    // rot = nad - adiff. (cos adiff, sin adiff) = (u_prev . u, u_prev x u) are at hand
-                    // (adiff is their atan2, wrapped into [-pi, pi]). For |nad| <= 0.0709 (every
-                    // adjustment of a step faster than 2.3 m/s: |nad| = nc / (50 speed), nc <= 8)
-                    // cos/sin of nad come from their Taylor polynomials (through x^8 / x^9: below
-                    // 1e-19 there), then the angle-difference formulas give cos/sin of rot within a
-                    // few ulp (the output frame only). Otherwise (and in k_cand<true>)
-                    // the library's sin/cos of rot; NaN/inf nad (speed 0) takes that path too.
-                    if (!kLarge && fabs(nad) <= 0.0709) {
-                        const double x2 = nad * nad;
-                        const double sn = __builtin_fma(nad * x2, __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2,
-                                              1.0 / 362880, -1.0 / 5040), 1.0 / 120), -1.0 / 6), nad);
-                        const double cn = __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2, __builtin_fma(x2,
-                                              1.0 / 40320, -1.0 / 720), 1.0 / 24), -0.5), 1.0);
-                        cr = cn * dt_st + sn * cr_st;
-                        sr = sn * dt_st - cn * cr_st;
-                    } else
-#endif
                     ppm::sincos_pp<kLarge>(rot, sr, cr);
-#endif
                     const double rvx = vx * cr - vy * sr;
                     const double rvy = vx * sr + vy * cr;
                     cx = tpx + rvx;
@@ -1752,7 +1292,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     double nad = kLarge ? nc / speed / 50
                                         : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
                     if (adiff < 0) nad *= -1;
-                    double* rp = rec_rot(rec - rs, rstride, P.n_points, ng, ws, rs);
+                    double* rp = rec_rot(rec - rs, rstride, ng, ws, rs);
                     if (PP_CHKP(rp, rec, nrec, 6))
                         PP_ST(rp, nad - adiff);   // rot (src/main.cpp:986)
                     const uint64_t bit = 1ull << (ng & 63);
@@ -1764,12 +1304,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         }
         cur_t += 0.02;
         prev_speed = speed;
-#if PP_ANGLE_CROSS
         uxp = ux; uyp = uy;
-#else
-        prev_angle = astep;
-#endif
-#if (PP_DIV_RCP & 1) && PP_ANGLE_CROSS && PP_STEP_FAST
         double sp_step, dpy;
         if (kLarge) {
             sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
@@ -1782,13 +1317,6 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (__builtin_expect(!dok, 0)) { sp_step = nx / d; dpy = ny / d; }
         }
         pos_y += dpy;
-#elif (PP_DIV_RCP & 1) && PP_ANGLE_CROSS
-        const double sp_step = ppm::div_rcp((x - pos_x) * dstep, d, rd);
-        pos_y += ppm::div_rcp((y - pos_y) * dstep, d, rd);
-#else
-        const double sp_step = (x - pos_x) * dstep / d;
-        pos_y += (y - pos_y) * dstep / d;
-#endif
         arg += sp_step;
         pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
         if (kOutMode != 0 && kOut) {
@@ -1798,7 +1326,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 st_xy(px + ng * ps, tx + cx, ty + cy);      // one 16-B store (x, y)
         }
-        if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, P.n_points, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, P.n_points, ng, ws, rs, pos_x, pos_y);
+        if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
@@ -1840,9 +1368,6 @@ __device__ __forceinline__ SC make_sc(const pp_params& P, const PrepV& pv, int64
     return sc;
 }
 
-#ifndef PP_CAND_CACHE
-#define PP_CAND_CACHE 1
-#endif
 
 // K4 inside k_cand (reference mode, emit_in): the winner lane of scene s replays the output
 // transform of its recorded path (src/main.cpp:994-1007, 1033-1037) with the sin/cos of each
@@ -1875,10 +1400,10 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
         for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, N, g, S, s), rec, nrec, 19); }
+            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, g, S, s), rec, nrec, 19); }
 #endif
             px_[u] = 0.0; py_[u] = 0.0;
-            if (g < ng) rec_ld(rec, rstride, N, g, S, s, px_[u], py_[u]);
+            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
         }
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
@@ -1913,12 +1438,6 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 // kMode 2: every candidate writes its path (emit_paths); 1: reference mode, the winner lanes
 // write next_x/next_y; 0: cost only (comfort mode; k_winner produces the outputs).
 // ------------------------------------------------------------------------------------------------
-#ifndef PP_CAND_WAVES
-#define PP_CAND_WAVES 4
-#endif
-#ifndef PP_CAND_WAVES_PATHS      // emit_paths instantiations (the output transform's registers)
-#define PP_CAND_WAVES_PATHS 4
-#endif
 // One group g of the candidate grid (BPS == 1: scenes [g SPB, g SPB + SPB); BPS > 1: candidates
 // [coff, coff + 256) of scene g / BPS) by the whole workgroup. Every barrier inside is reached by
 // all threads of the block (the early return is block-uniform).
@@ -1967,7 +1486,6 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         if (pv.lim_mask[(s0 + q) * D + (t - q * D)] & kLimSlow) { atomicOr(&sSlow[q], 1u); mine = true; }
     }
     if (!__syncthreads_or(mine) && kSlow) return;      // whole block leaves: no flagged scene
-#if PP_TEAM_SETUP
     {   // phase A: a team of TS threads per slot (team_a1..a5), block barriers between the steps
         int TS = (int)blockDim.x / nslot;
         if (TS > 8) TS = 8;
@@ -1979,7 +1497,6 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         LaneGeom g;
         if (act) { g = lane_geom(pv, s * D, Sv, L); team_a1(m, in, g, s, L, sl, r, TS); }
         __syncthreads();
-#if PP_SERIAL_WAVE
         // the two serial steps (A2, A4) on one lane per slot, slots in lane order: NL * SPB <= 64
         // slots fit the block's first wave, whose instruction stream is then the only one paying
         // for them (a team layout spreads them over every wave of the block)
@@ -1994,35 +1511,14 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             gs.pos_x = pv.pos_x[vs]; gs.pos_y = pv.pos_y[vs]; gs.ego_d = pv.ego_d[vs];
             team_a2(gs, sls);
         }
-#else
-        if (act && r == 0) team_a2(g, sl);
-#endif
         __syncthreads();
-#ifndef PP_ABL_A
-#define PP_ABL_A 0
-#endif
-        if (!(PP_ABL_A & 4) && act) team_a3(sl, r, TS);   // PP_ABL_A: diagnostic timing builds
+        if (act) team_a3(sl, r, TS);
         __syncthreads();
-#if PP_SERIAL_WAVE
-        if (!(PP_ABL_A & 2) && act_s) team_a4(sls);
-#else
-        if (!(PP_ABL_A & 2) && act && r == 0) team_a4(sl);
-#endif
+        if (act_s) team_a4(sls);
         __syncthreads();
-        if (!(PP_ABL_A & 4) && act) team_a5(sl, r, TS);
+        if (act) team_a5(sl, r, TS);
     }
-#else
-    if (tid < NL * nsc && ((sSlow[tid / NL] != 0) == kSlow)) {   // phase A
-        const int j = tid;
-        const Slot sl = lds_slot(sX, nslot, sMeta, j);
-        setup_lane(m, P, in, pv, s0 + j / NL, (s0 + j / NL) * D, Sv, j % NL, sl);
-    }
-#endif
     __syncthreads();
-#ifdef PP_ABL_NO_PHASE_B   // diagnostic timing build: phase A only
-    if (tid < nsc) out.status[s0 + tid] = 0;
-    return;
-#endif
     // Lane -> candidate. Reference mode without draws (kMode 1): lanes [0, nsc) run the scenes'
     // winning candidates (planner lane T, max_speed: known from k_prep) and record their paths;
     // lanes >= nsc run the C - 1 other candidates of each scene cost-only. The output work is
@@ -2086,7 +1582,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 st_xy(p0 + i * ps, in.prev_x[(int64_t)i * S + s], in.prev_y[(int64_t)i * S + s]);
             }
             double* px = p0 + K * ps;
-            R = run_candidate<kSlow, 2, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
+            R = run_candidate<kSlow, 2>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
                                                        pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
                                                        px, ps);
             for (int i = R.ng; i < N - K; i++) {
@@ -2102,41 +1598,10 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
             }
-#ifdef PP_ABL_NO_REC       // diagnostic timing build: the first wave runs the cost-only loop too
-#define PP_REC_WAVE false
-#else
-#define PP_REC_WAVE (kMode == 1 && tid < 64)
-#endif
-        } else if (PP_REC_WAVE && PP_WIN_INLINE && !emit_in) {
-            // reference mode, the block's first wave: the winners transform their path as they
-            // walk it and write next_x/next_y (the kept previous points first, zeros after the
-            // last point); the other lanes of the wave are cost-only
-            double* wx = nullptr;
-            double* wy = nullptr;
-            if (winner) {
-                for (int i = 0; i < K; i++) {
-                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 9)) break;
-                    out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
-                    out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
-                }
-                wx = out.next_x + (int64_t)K * S + s;
-                wy = out.next_y + (int64_t)K * S + s;
-            }
-            R = run_candidate<kSlow, 1, PP_CAND_CACHE>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
-                                                       pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
-                                                       nullptr, 0, winner);
-            if (winner) {
-                for (int i = K + R.ng; i < N; i++) {
-                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 10)) break;
-                    out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0;
-                }
-                out.n_out[s] = K + R.ng;
-                out.winner[s] = c;
-            }
-        } else if (PP_REC_WAVE) {
+        } else if (kMode == 1 && tid < 64) {
             // reference mode, the block's first wave: the winners record their local path
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
-            R = run_candidate<kSlow, 3, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
+            R = run_candidate<kSlow, 3>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
                                                        S, nullptr, 0, winner, rec + s, 0, s);
             if (winner && emit_in) {          // in-block K4 below: step count and masks in LDS
                 out.n_out[s] = K + R.ng;
@@ -2149,7 +1614,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 adjm[S + s] = R.adj1;
             }
         } else {
-            R = run_candidate<kSlow, 0, PP_CAND_CACHE>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
+            R = run_candidate<kSlow, 0>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
                                                        nullptr, nullptr, 0, nullptr, 0, true, nullptr,
                                                        fabs(sc.target - sc.start) >= 7.5 * sc.ttime ? 2 : (sc.target > sc.start ? 1 : 0));
         }
@@ -2179,7 +1644,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             const uint64_t mm = gs < 64 ? sAdj[2 * w] : sAdj[2 * w + 1];
             if (!((mm >> (gs & 63)) & 1)) continue;
             const int64_t s = s0 + w;
-            const double* rr = rec_rot(rec, (int64_t)(N - pv.K[s]) * S, N, gs, S, s);
+            const double* rr = rec_rot(rec, (int64_t)(N - pv.K[s]) * S, gs, S, s);
             if (!PP_CHKP(rr, rec, nrec, 18)) continue;
             const double rt = *rr;
             double sr, cr;
@@ -2190,7 +1655,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         __syncthreads();
         if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
             const int64_t s = s0 + tid;
-            emit_scene_pre<PP_EMIT_CHUNK>(in, P, pv, out, rec, s, pv.K[s], sNg[tid], sAdj[2 * tid],
+            emit_scene_pre<kEmitChunk>(in, P, pv, out, rec, s, pv.K[s], sNg[tid], sAdj[2 * tid],
                                           sAdj[2 * tid + 1], pcr + tid * N, psr + tid * N);
         }
     }
@@ -2202,17 +1667,11 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 // are block-uniform; a barrier separates consecutive groups' use of the block's LDS). Each group
 // clears its bit after use, so the bitmap is all zero again for the next pp_eval.
 template <bool kSlow, int kMode>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES_PATHS : PP_CAND_WAVES))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kCandWaves))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
                                               uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
                                               const uint32_t* gcount, int64_t g0) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-#ifndef PP_PRIO
-#define PP_PRIO 0
-#endif
-    // PP_PRIO (experiment): issue priority of the block's first wave, which carries the serial
-    // phase-A steps and the winners' longer recording body that the block's LDS waits for
-    if (PP_PRIO > 0 && threadIdx.x < 64) __builtin_amdgcn_s_setprio(PP_PRIO);
     if (!kSlow) {
         cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g0 + blockIdx.x, sm);
         return;
@@ -2221,7 +1680,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 
     const uint32_t nl = *gcount;                                  // same address for every lane
     for (uint32_t i = blockIdx.x; i < nl; i += gridDim.x) {
         const int64_t g = glist[i];
-        if (g >= ngroups) continue;                               // (never: k_prep lists this call's groups)
+        if (!PP_CHK(g < ngroups, 21, g)) continue;               // (never: k_prep lists this call's groups)
         __syncthreads();                                          // the previous group's LDS readers are done
         cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
@@ -2278,7 +1737,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
         out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
         out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
     }
-    const CandRes R = run_candidate<kSlow, 2, true>(P, sl, pv.pos_x[v0], pv.pos_y[v0], pv.angle[v0],
+    const CandRes R = run_candidate<kSlow, 2>(P, sl, pv.pos_x[v0], pv.pos_y[v0], pv.angle[v0],
                                                     pv.ca_p[v0], pv.sa_p[v0], sc, N - K,
                                                     out.next_x + (int64_t)K * S + s,
                                                     out.next_y + (int64_t)K * S + s, S, nullptr, 0);
@@ -2294,7 +1753,7 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
 // (src/main.cpp:994-1007), every point is mapped back with the current frame (:1033-1037). One lane
 // per scene; all loads/stores point-major (coalesced).
 // ------------------------------------------------------------------------------------------------
-// kChunk: recorded steps loaded together per lane (PP_EMIT_CHUNK for large batches; small batches,
+// kChunk: recorded steps loaded together per lane (kEmitChunk for large batches; small batches,
 // where the kernel is one serial chain of memory round trips per lane, load 16 steps at a time)
 template <int kChunk>
 __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_params& P, const PrepV& pv,
@@ -2319,7 +1778,6 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     double ca = pv.ca_p[s], sa = pv.sa_p[s];
     const uint64_t m0 = adjm[s], m1 = adjm[S + s];
     double pxp = 0, pyp = 0;                       // local position before the step
-#if PP_EMIT_ROTATE
     // The adjusted steps are sparse and scattered over the wave's lanes, so the rotation block
     // runs, with few lanes active, on most steps: it is kept short. The heading's sin/cos follow
     // by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead of sin/cos of the
@@ -2350,12 +1808,12 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
             const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
             bits |= bit ? 1u << u : 0u;
 #ifdef PP_CHECK
-            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, N, g, S, s), rec, nrec, 16); }
-            if (bit) { PP_CHKP(rec_rot(rec, rstride, N, g, S, s), rec, nrec, 16); }
+            if (g < ng) { PP_CHKP(rec_py((double*)rec, rstride, g, S, s), rec, nrec, 16); }
+            if (bit) { PP_CHKP(rec_rot(rec, rstride, g, S, s), rec, nrec, 16); }
 #endif
             px_[u] = 0.0; py_[u] = 0.0;
-            if (g < ng) rec_ld(rec, rstride, N, g, S, s, px_[u], py_[u]);
-            rt[u] = bit ? PP_LD(rec_rot(rec, rstride, N, g, S, s)) : 0.0;
+            if (g < ng) rec_ld(rec, rstride, g, S, s, px_[u], py_[u]);
+            rt[u] = bit ? PP_LD(rec_rot(rec, rstride, g, S, s)) : 0.0;
         }
         bool huge = false;
 #pragma unroll
@@ -2363,13 +1821,13 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         if (__builtin_expect(huge, 0)) {
             for (int g = g0; g < ng && g < g0 + kEmitChunk; g++) {
                 if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
-                    const double rot = *rec_rot(rec, rstride, N, g, S, s);
+                    const double rot = *rec_rot(rec, rstride, g, S, s);
                     double cr, sr;
                     ppm::sincos_pp<true>(rot, sr, cr);
                     rotate(rot, cr, sr);
                 }
                 double qx, qy;
-                rec_ld(rec, rstride, N, g, S, s, qx, qy);
+                rec_ld(rec, rstride, g, S, s, qx, qy);
                 out.next_x[(int64_t)(K + g) * S + s] = (qx * ca - qy * sa) + cx;
                 out.next_y[(int64_t)(K + g) * S + s] = (qx * sa + qy * ca) + cy;
                 pxp = qx;
@@ -2380,17 +1838,9 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         // sin/cos of the chunk's turns first (rt = 0 where no turn): independent of each other and
         // of the chain of turns below, so they overlap instead of queueing behind it
         double crs[kEmitChunk], srs[kEmitChunk];
-#ifdef PP_ABL_EMIT_NOROT    // diagnostic timing build (wrong results): no turn is replayed
-        bits = 0;
-#endif
         if (bits) {
-#ifdef PP_ABL_EMIT_TRIG     // diagnostic timing build (wrong results): first-order sin/cos of the turns
-#pragma unroll
-            for (int u = 0; u < kEmitChunk; u++) { srs[u] = rt[u]; crs[u] = 1.0; }
-#else
 #pragma unroll
             for (int u = 0; u < kEmitChunk; u++) ppm::sincos_pp<false>(rt[u], srs[u], crs[u]);
-#endif
         }
 #pragma unroll
         for (int u = 0; u < kEmitChunk; u++) {
@@ -2407,43 +1857,11 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         }
     }
     (void)tangle;
-#else
-    for (int g = 0; g < ng; g++) {
-        const uint64_t bit = g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1;
-        if (bit) {
-            const double rot = *rec_rot(rec, rstride, N, g, S, s);
-            double tpx = pxp * ca - pyp * sa;
-            double tpy = pxp * sa + pyp * ca;
-            tpx = tpx + cx;
-            tpy = tpy + cy;
-            const double vx = cx - tpx, vy = cy - tpy;
-            double cr, sr;
-            ppm::sincos_pp<true>(rot, sr, cr);
-            const double rvx = vx * cr - vy * sr;
-            const double rvy = vx * sr + vy * cr;
-            cx = tpx + rvx;
-            cy = tpy + rvy;
-            tangle += rot;
-            ppm::sincos_pp<true>(tangle, sa, ca);
-        }
-        double px_, py_;
-        rec_ld(rec, rstride, N, g, S, s, px_, py_);
-        const double tx = px_ * ca - py_ * sa;
-        const double ty = px_ * sa + py_ * ca;
-        out.next_x[(int64_t)(K + g) * S + s] = tx + cx;
-        out.next_y[(int64_t)(K + g) * S + s] = ty + cy;
-        pxp = px_;
-        pyp = py_;
-    }
-#endif
     for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
 }
 
 template <int kChunk>
-#ifndef PP_EMIT_WAVES            // k_emit occupancy (waves per SIMD); 0: the compiler's choice
-#define PP_EMIT_WAVES 0
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PP_EMIT_WAVES > 0 ? PP_EMIT_WAVES : 1))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                               const double* rec, const uint64_t* adjm, int64_t s0, int64_t s1) {
     const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // scenes [s0, s1)
     if (s >= s1 || s >= in.n_scenes) return;
@@ -2698,8 +2116,6 @@ struct StreamWS {
     int64_t rec_cap = 0;
     uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
     int64_t gbits_cap = 0;        // words
-    hipStream_t aux = nullptr;    // the chunked pipeline's second stream (K1 and K4 of other chunks)
-    std::vector<hipEvent_t> sev;  // its synchronisation events
 };
 struct DevState {
     bool init = false;
@@ -2883,47 +2299,29 @@ PrepV prep_bind(void* base, int64_t S) {
     return p;
 }
 
-// K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
-// SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. pp_set_prep_group (or
-// the PP_PREP_G environment variable) forces a value.
-// K4 inside k_cand: the winners' sin/cos tables (2 N doubles each) fit the block's spline slots;
-// PP_EMIT_IN=0 forces the k_emit kernel (A/B, tests)
-bool emit_in_ok(int N) {
-    const char* e = getenv("PP_EMIT_IN");
-    if (e && *e && atoi(e) == 0) return false;
-    return 2 * N <= 5 * NL * kKP;
-}
-// k_cand_small (K2 + K4 in one launch) up to this many scenes; PP_FUSED=0/1 forces it off/on (A/B)
+// pp_debug_set's switches (include/pp.h PP_DBG_*): launch-shape overrides for tests and A/B
+// measurements. Every one defaults to 0 = the product's own choice; nothing reads the environment.
+std::atomic<int> g_dbg[PP_DBG_KEYS];
+int dbg(int key) { return g_dbg[key].load(std::memory_order_relaxed); }
+
+// K4 inside k_cand: the winners' sin/cos tables (2 N doubles each) fit the block's spline slots
+bool emit_in_ok(int N) { return 2 * N <= 5 * NL * kKP; }
+// small reference-mode batches (<= kFusedSmall scenes): K2 + K4 in one launch (k_cand_small) or the
+// whole step in one launch (k_step_small); PP_DBG_SHAPE forces one of the three shapes
 constexpr int64_t kFusedSmall = 16384;
 bool fused_small(int64_t S) {
-    const char* e = getenv("PP_FUSED");
-    return e && *e ? atoi(e) != 0 : S <= kFusedSmall;
+    const int f = dbg(PP_DBG_SHAPE);
+    return f ? f != PP_SHAPE_SPLIT : S <= kFusedSmall;
 }
-// k_prep_st (cars staged in LDS): its LDS (map, then 16-B aligned (x, y) pairs and the match words).
-// Off by default: it reads the scene record once (FETCH 0.57 GB raw per 2M-scene launch against
-// the gathering k_prep's 4.0 GB, whose re-reads the Infinity Cache serves) but its LDS allows 2 waves
-// per SIMD instead of 3, and it takes 2.75 ms against 2.05. PP_PREP_ST=1 selects it.
-constexpr size_t kLdsMaxBlock = 163840;
-size_t prep_st_lds(int n) {
-    return sizeof(double) * (size_t)((kMapArrays * n + 1) & ~1) + (16 + 4) * (size_t)kStRows * kStBlock;
-}
-bool prep_st_on() {
-    const char* e = getenv("PP_PREP_ST");
-    return e && *e ? atoi(e) != 0 : false;
-}
-// k_step_small (K1 + K2 + K4 in one launch for the batches k_cand_small takes); PP_STEP_FUSED=0
-// falls back to k_prep_g* + k_cand_small (A/B, tests)
-bool step_fused_on() {
-    const char* e = getenv("PP_STEP_FUSED");
-    return e && *e ? atoi(e) != 0 : true;
-}
+bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
 // 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
 // scenes: 2.07 ms for 32,768 waves at 3, 2.29 ms at 4); 262,144 scenes (BASELINE config 5 over 8
-// GPUs) = 4,096 waves = 1.33 rounds at 3 (0.352 ms measured) or exactly 1 at 4. PP_PREP_W4=0/1.
+// GPUs) = 4,096 waves = 1.33 rounds at 3 (0.352 ms measured) or exactly 1 at 4. PP_DBG_PREP_WAVES
+// forces 3 or 4.
 bool prep_w4(int64_t Sv, int device) {
-    const char* e = getenv("PP_PREP_W4");
-    if (e && *e) return atoi(e) != 0;
+    const int f = dbg(PP_DBG_PREP_WAVES);
+    if (f == 3 || f == 4) return f == 4;
     static int cus[kMaxDev] = {};
     if (device < 0 || device >= kMaxDev) return false;
     if (cus[device] == 0) {
@@ -2935,57 +2333,19 @@ bool prep_w4(int64_t Sv, int device) {
     const int64_t r3 = (waves + 3 * simds - 1) / (3 * simds), r4 = (waves + 4 * simds - 1) / (4 * simds);
     return 286 * r4 < 188 * r3;
 }
-// pp_eval's two-stream pipeline: chunks of the k_cand groups for batches of at least kPipeMin scenes
-// (PP_CHUNKS=n forces n chunks, 1 = off; at most kMaxChunks, and at least 64 groups per chunk)
-constexpr int64_t kPipeMin = 131072;
-constexpr int kMaxChunks = 16;
-#ifndef PP_PIPE_CHUNKS
-#define PP_PIPE_CHUNKS 1
-#endif
-// PP_SPLIT=n (experiment): n chunks, each a whole K1 -> K2 -> K4 pipeline of its own, chunks
-// alternating between the caller's stream and the auxiliary one (no event between the streams
-// until the join), instead of the K2-on-one-stream pipeline above
-int pipe_split() {
-    const char* e = getenv("PP_SPLIT");
-    return e && *e ? atoi(e) : 0;
-}
-int pipe_chunks(int64_t S, int64_t groups) {
-    const char* e = getenv("PP_CHUNKS");
-    const int sp = pipe_split();
-    int n = sp > 1 ? sp : e && *e ? atoi(e) : (S >= kPipeMin ? PP_PIPE_CHUNKS : 1);
-    if (n > kMaxChunks) n = kMaxChunks;
-    while (n > 1 && groups < 64LL * n) n--;
-    return n < 1 ? 1 : n;
-}
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
-std::atomic<int> g_prep_forced{-1};     // pp_set_prep_group; -1: not yet read from PP_PREP_G
+// K1 lanes per evaluation: the largest power of two <= 16 that keeps Sv * G within ~2 waves per
+// SIMD of the chip (256 CUs x 4 SIMDs x 64 lanes x 2); 1 for large batches. PP_DBG_PREP_GROUP
+// forces a value.
 bool prep_group_ok(int G) { return G == 0 || G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
 int prep_group(int64_t Sv) {
-    int forced = g_prep_forced.load(std::memory_order_relaxed);
-    if (forced < 0) {
-        const char* e = getenv("PP_PREP_G");
-        forced = e && prep_group_ok(atoi(e)) ? atoi(e) : 0;
-        int expect = -1;
-        g_prep_forced.compare_exchange_strong(expect, forced);
-        forced = g_prep_forced.load(std::memory_order_relaxed);
-    }
+    const int forced = dbg(PP_DBG_PREP_GROUP);
     if (forced > 0) return forced;
     const int64_t target = 256LL * 4 * 64 * 2;
     int G = 1;
     while (G < 16 && Sv * G * 2 <= target) G *= 2;
     return G;
-}
-
-// k_prep's dynamic LDS (map + the flattened car pass's words) may pass 64 KB (maps of 400+
-// waypoints): allow one workgroup the whole 160 KB, once per process
-void prep_lds_attr() {
-    static std::once_flag once;
-    std::call_once(once, [] {
-        const void* f[4] = {(const void*)k_prep<true, false>, (const void*)k_prep<true, true>,
-                            (const void*)k_prep<false, false>, (const void*)k_prep<false, true>};
-        for (const void* k : f) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMaxBlock);
-    });
 }
 
 int cands_per_block(int C) {
@@ -3013,15 +2373,14 @@ int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
     return PP_OK;
 }
 
-// The slow-group bitmap (words), then the flagged-group counts (one per pipeline chunk) and list
-// (ngroups entries; chunk c's entries from its first group on), in one allocation:
-// [cap words][kMaxChunks counts][list: 32 cap entries]
+// The slow-group bitmap (words), then the flagged-group count and list (ngroups entries), in one
+// allocation: [cap words][count][list: 32 cap entries]
 int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     const int64_t words = (ngroups + 31) / 32;
     if (W.gbits_cap >= words) return PP_OK;
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
-    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + kMaxChunks + 32 * cap);
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 1 + 32 * cap);
     if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
@@ -3032,20 +2391,7 @@ void free_ws(StreamWS& W) {
     if (W.ws) (void)hipFree(W.ws);
     if (W.rec) (void)hipFree(W.rec);
     if (W.gbits) (void)hipFree(W.gbits);
-    for (hipEvent_t e : W.sev) (void)hipEventDestroy(e);
-    if (W.aux) (void)hipStreamDestroy(W.aux);
     W = StreamWS();
-}
-
-// the chunked pipeline's stream and at least n synchronisation events (callers hold M->mu)
-int ensure_aux(StreamWS& W, size_t n) {
-    if (!W.aux && hipStreamCreateWithFlags(&W.aux, hipStreamNonBlocking) != hipSuccess) { W.aux = nullptr; return PP_ERR_HIP; }
-    while (W.sev.size() < n) {
-        hipEvent_t e;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
-        W.sev.push_back(e);
-    }
-    return PP_OK;
 }
 
 // k_cand's launch geometry for C candidates per scene (BPS == 1: SPB scenes per group; else one
@@ -3311,14 +2657,29 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         rec = rec_buf(W.rec);
         adjm = adj_buf(W.rec, W.rec_cap);
     }
-    {   // PP_POISON_WS=1 (test builds' switch, read once): every call starts from a NaN-filled prep
-        // workspace and winner record, so no kernel can lean on what an earlier call left there
-        static const bool poison = [] { const char* e = getenv("PP_POISON_WS"); return e && *e == '1'; }();
-        if (poison) {
-            if (hipMemsetAsync(W.ws, 0xFF, prep_bytes(W.ws_cap), st) != hipSuccess) return PP_ERR_HIP;
-            if (rec && hipMemsetAsync(rec, 0xFF, sizeof(double) * 3 * PP_MAX_POINTS * (size_t)W.rec_cap, st) != hipSuccess)
-                return PP_ERR_HIP;
-        }
+    if (dbg(PP_DBG_POISON)) {
+        // every call starts from NaN-filled (0xFF) intermediates and outputs, so no kernel can lean
+        // on what an earlier call left there (or on an output element it never writes); the
+        // slow-group bitmap must be all zero between calls (k_cand<true> clears what k_prep set)
+        auto fill = [&](void* p, size_t bytes) { return !p || !bytes || hipMemsetAsync(p, 0xFF, bytes, st) == hipSuccess; };
+        const int64_t Cn = (int64_t)Dn * NL * prm->n_speeds, N = prm->n_points;
+        const int64_t words = (cg.groups + 31) / 32;
+        std::vector<uint32_t> hb((size_t)words);
+        if (hipMemcpyAsync(hb.data(), W.gbits, sizeof(uint32_t) * words, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return PP_ERR_HIP;
+        for (uint32_t w : hb)
+            if (w) return PP_ERR_STATE;
+        const bool ok = fill(W.ws, prep_bytes(W.ws_cap)) &&
+                        fill(W.rec, W.rec ? rec_bytes(W.rec_cap) : 0) &&
+                        fill(W.gbits + W.gbits_cap + 1, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
+                        fill(out->winner, 4 * S) && fill(out->n_out, 4 * S) && fill(out->status, 4 * S) &&
+                        fill(out->next_x, 8 * N * S) && fill(out->next_y, 8 * N * S) &&
+                        fill(out->cost, 8 * Cn * S) && fill(out->info, sizeof(pp_scene_info) * S) &&
+                        fill(out->draw_mean_cost, Dn > 1 ? 8 * NL * prm->n_speeds * S : 0) &&
+                        fill(prm->emit_paths ? out->paths : nullptr, 16 * N * Cn * S) &&
+                        fill(prm->emit_paths ? out->path_len : nullptr, 4 * Cn * S);
+        if (!ok) return PP_ERR_HIP;
     }
     const PrepV pv = prep_bind(W.ws, W.ws_cap);
     MapG mg;
@@ -3347,7 +2708,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     gb.count = W.gbits + W.gbits_cap;
-    gb.list = gb.count + kMaxChunks;
+    gb.list = gb.count + 1;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -3378,99 +2739,6 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
-    // Large reference-mode batches: a two-stream pipeline over chunks of the k_cand groups. The
-    // caller's stream runs only K2 (chunk after chunk); the second stream runs K1 of chunk c + 1
-    // and K4 of chunk c - 1 meanwhile, so the latency-bound K1 and the memory-bound K4 fill what
-    // the VALU-bound K2 leaves idle. Same kernels, same arithmetic, per-chunk
-    // ranges: the results are those of the one-chunk launch, bit for bit (tests/test_pipeline.py).
-    const int nch = pipe_chunks(S, cg.groups);
-    if (nch > 1 && ref_direct && !P.emit_paths && cg.bps == 1 && Dn == 1 && prep_group(Sv) == 1 &&
-        !prep_st_on() && !PP_WIN_INLINE) {
-        rc = ensure_aux(W, 2 * (size_t)nch + 2);
-        if (rc) return rc;
-        hipStream_t ax = W.aux;
-        hipEvent_t* pe = W.sev.data();               // pe[c]: K1 of chunk c done
-        hipEvent_t* ce = pe + nch;                   // ce[c]: K2 of chunk c done
-        hipEvent_t e_start = W.sev[2 * nch], e_done = W.sev[2 * nch + 1];
-        const bool lmap = mg.n <= kLdsMapMax;
-        const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
-        int64_t gstep = (cg.groups + nch - 1) / nch;
-        gstep = (gstep + 63) / 64 * 64;              // chunk boundaries on 64-group (32-bit word, 64-scene-multiple) edges
-        auto g_lo = [&](int c) { return std::min<int64_t>((int64_t)c * gstep, cg.groups); };
-        auto s_lo = [&](int c) { return std::min<int64_t>(g_lo(c) * cg.spb, S); };
-        prep_lds_attr();
-        auto prep = [&](int c, hipStream_t ax) {
-            GroupBits gc = gb;
-            gc.count = gb.count + c;
-            gc.list = gb.list + g_lo(c);
-            const int64_t v0 = s_lo(c), v1 = s_lo(c + 1);
-            if (v1 <= v0) return;
-            const unsigned blocks = (unsigned)((v1 - v0 + 255) / 256);
-            if (prep_w4(v1 - v0, device)) {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(blocks), dim3(256), lds + kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, true>), dim3(blocks), dim3(256), kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-            } else {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(blocks), dim3(256), lds + kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, false>), dim3(blocks), dim3(256), kPrepLdsFlat, ax, mg, B, P, pv, R.info, R.status, gc, v0, v1);
-            }
-        };
-        auto emit = [&](int c, hipStream_t ax) {
-            const int64_t s0 = s_lo(c), s1 = s_lo(c + 1);
-            if (s1 <= s0) return;
-            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)((s1 - s0 + 255) / 256)), dim3(256), 0, ax, B, P,
-                               pv, R, rec, adjm, s0, s1);
-        };
-        if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t) * nch, st) != hipSuccess) return PP_ERR_HIP;
-        if (timing) (void)hipEventRecord(ev[0], st);
-        if (hipEventRecord(e_start, st) != hipSuccess || hipStreamWaitEvent(ax, e_start, 0) != hipSuccess) return PP_ERR_HIP;
-        if (pipe_split() > 1) {      // whole pipelines per chunk, alternating streams (timing: all in "k_cand")
-            if (timing) (void)hipEventRecord(ev[1], st);
-            const char* stg = getenv("PP_SPLIT_STAGGER");
-            const int stagger = stg && *stg ? atoi(stg) : 0;
-            for (int c = 0; c < nch; c++) {
-                hipStream_t sc = (c & 1) ? ax : st;
-                // stagger 1: chunk c starts after chunk c - 1's K1 (its K2 then runs beside the other
-                // stream's K2 tail and K4); 2: after chunk c - 1's K2
-                if (stagger && c > 0 && hipStreamWaitEvent(sc, pe[c - 1], 0) != hipSuccess) return PP_ERR_HIP;
-                prep(c, sc);
-                if (stagger == 1 && hipEventRecord(pe[c], sc) != hipSuccess) return PP_ERR_HIP;
-                const int64_t g0 = g_lo(c), g1 = g_lo(c + 1);
-                if (g1 > g0) {
-                    hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sc, mg, B, P, pv, R,
-                                       cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
-                    hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)std::min<int64_t>(g1 - g0, 2048)), dim3(cg.threads), cg.lds, sc,
-                                       mg, B, P, pv, R, cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
-                }
-                if (stagger == 2 && hipEventRecord(pe[c], sc) != hipSuccess) return PP_ERR_HIP;
-                emit(c, sc);
-            }
-            if (hipEventRecord(e_done, ax) != hipSuccess || hipStreamWaitEvent(st, e_done, 0) != hipSuccess) return PP_ERR_HIP;
-            if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
-            if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
-            return PP_OK;
-        }
-        for (int c = 0; c < 2 && c < nch; c++) { prep(c, ax); if (hipEventRecord(pe[c], ax) != hipSuccess) return PP_ERR_HIP; }
-        for (int c = 0; c < nch; c++) {
-            if (hipStreamWaitEvent(st, pe[c], 0) != hipSuccess) return PP_ERR_HIP;
-            if (c == 0 && timing) (void)hipEventRecord(ev[1], st);
-            const int64_t g0 = g_lo(c), g1 = g_lo(c + 1);
-            if (g1 > g0) {
-                hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
-                                   cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
-                hipLaunchKernelGGL((k_cand<true, 1>), dim3((unsigned)std::min<int64_t>(g1 - g0, 2048)), dim3(cg.threads), cg.lds, st,
-                                   mg, B, P, pv, R, cg.spb, cg.bps, rec, adjm, W.gbits, cg.groups, gb.list + g0, gb.count + c, g0);
-            }
-            if (hipEventRecord(ce[c], st) != hipSuccess || hipStreamWaitEvent(ax, ce[c], 0) != hipSuccess) return PP_ERR_HIP;
-            emit(c, ax);
-            if (c + 2 < nch) { prep(c + 2, ax); if (hipEventRecord(pe[c + 2], ax) != hipSuccess) return PP_ERR_HIP; }
-        }
-        if (timing) (void)hipEventRecord(ev[2], st);
-        if (hipEventRecord(e_done, ax) != hipSuccess || hipStreamWaitEvent(st, e_done, 0) != hipSuccess) return PP_ERR_HIP;
-        if (timing) (void)hipEventRecord(ev[3], st);
-        if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
-        return PP_OK;
-    }
-    prep_lds_attr();
     if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
@@ -3478,37 +2746,23 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         const int G = prep_group(Sv);
         const int64_t blocks = (Sv * G + threads - 1) / threads;
         if (timing) (void)hipEventRecord(ev[0], st);
-#ifdef PP_PREP_GMAP   // diagnostic timing build: k_prep reads the map through L1/L2 at any size
-        const bool lmap = false;
-#else
         const bool lmap = mg.n <= kLdsMapMax;
-#endif
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
 #define PP_LAUNCH_PREP(KER) \
         if (lmap) hipLaunchKernelGGL(KER<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb); \
         else hipLaunchKernelGGL(KER<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb)
-        const size_t lds_st = prep_st_lds(mg.n);
-        if (G == 1 && !B.tab_valid && lmap && B.car_stride <= kStRows && lds_st <= kLdsMaxBlock &&
-            prep_st_on()) {
-            static std::once_flag attr_once;     // dynamic LDS beyond 64 KB (one workgroup may hold 160 KB)
-            std::call_once(attr_once, [] {
-                (void)hipFuncSetAttribute((const void*)k_prep_st<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)kLdsMaxBlock);
-            });
-            hipLaunchKernelGGL(k_prep_st<0>, dim3((unsigned)((Sv + kStBlock - 1) / kStBlock)), dim3(kStBlock),
-                               lds_st, st, mg, B, P, pv, R.info, R.status, gb);
-        } else switch (G) {
+        switch (G) {
             case 2: { PP_LAUNCH_PREP(k_prep_g2); break; }
             case 4: { PP_LAUNCH_PREP(k_prep_g4); break; }
             case 8: { PP_LAUNCH_PREP(k_prep_g8); break; }
             case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
             default: {
                 if (prep_w4(Sv, device)) {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds + kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 } else {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds + kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), kPrepLdsFlat, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 }
                 break;
             }
@@ -3537,13 +2791,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     }
     if (timing) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
-    if (ref_direct && !P.emit_paths && !emit_in && !PP_WIN_INLINE) {
+    if (ref_direct && !P.emit_paths && !emit_in) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
             const int64_t blocks = (S + 63) / 64;
             hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         } else {
             const int64_t blocks = (S + 255) / 256;
-            hipLaunchKernelGGL(k_emit<PP_EMIT_CHUNK>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
+            hipLaunchKernelGGL(k_emit<kEmitChunk>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         }
     }
     // K3 (comfort mode, or any mode with draws): argmin + winner path
@@ -3557,11 +2811,21 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     return PP_OK;
 }
 
-int32_t pp_set_prep_group(int32_t lanes) {
-    if (!prep_group_ok(lanes)) return PP_ERR_ARG;
-    g_prep_forced.store(lanes, std::memory_order_relaxed);
+int32_t pp_debug_set(int32_t key, int32_t value) {
+    bool ok = false;
+    switch (key) {
+        case PP_DBG_PREP_GROUP: ok = prep_group_ok(value); break;
+        case PP_DBG_PREP_WAVES: ok = value == 0 || value == 3 || value == 4; break;
+        case PP_DBG_SHAPE: ok = value >= 0 && value <= PP_SHAPE_STEP; break;
+        case PP_DBG_POISON: ok = value == 0 || value == 1; break;
+        default: break;
+    }
+    if (!ok) return PP_ERR_ARG;
+    g_dbg[key].store(value, std::memory_order_relaxed);
     return PP_OK;
 }
+
+int32_t pp_debug_get(int32_t key) { return key >= 0 && key < PP_DBG_KEYS ? dbg(key) : PP_ERR_ARG; }
 
 int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
     if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
@@ -3832,6 +3096,10 @@ int32_t pp_plan_batch_host(pp_map* M, int32_t device, pp_scene_batch* hin, const
     if (!ok) return PP_ERR_HIP;
     int rc = pp_eval(M, &B, prm, &R, device, hip_stream);
     if (rc != PP_OK) return rc;
+    if (small && dbg(PP_DBG_POISON)) {   // the mirror's pure-output regions (inputs may still be in flight)
+        memset(mirror + ((const char*)nxy - base), 0xFF, (size_t)(d_out_end - (const char*)nxy));
+        memset(mirror + ((const char*)outi - base), 0xFF, (size_t)(i_out_end - (const char*)outi));
+    }
     if (small) {
         copy(d_out_beg, d_out_end, false);
         copy(i_out_beg, i_out_end, false);
@@ -3913,6 +3181,12 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     }
     Frame& h = *(Frame*)DS.frame_host;
     memset(&h, 0, sizeof(h));
+    const bool poison = dbg(PP_DBG_POISON) != 0;
+    if (poison) {     // the outputs' staging starts NaN-filled (pp_eval poisons them on the device too)
+        memset(h.nx, 0xFF, sizeof h.nx); memset(h.ny, 0xFF, sizeof h.ny); memset(h.cost, 0xFF, sizeof h.cost);
+        memset(&h.winner, 0xFF, sizeof h.winner); memset(&h.nout, 0xFF, sizeof h.nout);
+        memset(&h.status, 0xFF, sizeof h.status); memset(&h.info, 0xFF, sizeof h.info);
+    }
     h.ego[0] = ego_x; h.ego[1] = ego_y; h.ego[2] = ego_yaw_deg; h.ego[3] = ego_speed_mph;
     for (int i = 0; i < PP_PREV_KEEP && i < n_prev; i++) { h.px[i] = prev_x[i]; h.py[i] = prev_y[i]; }
     h.nprev = n_prev; h.ptl = *target_lane; h.ncars = nc;
@@ -3921,7 +3195,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     }
     // the reference's std::map, laid out over the union of its ids and this frame's (any ints)
     const pptab::Slots hs = {1, h.tid, h.tvalid, h.tlane, h.ts, h.td, h.tvs, h.tvd, h.tvx, h.tvy};
-    const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS);
+    const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS, poison);
     if (nslots < 0) return PP_ERR_ARG;                  // more than PP_MAX_CARS distinct cars
     hipStream_t st = DS.frame_stream;
     if (hipMemcpyAsync(d, &h, sizeof(Frame), hipMemcpyHostToDevice, st) != hipSuccess) return PP_ERR_HIP;

@@ -16,17 +16,10 @@ namespace ppm {
 // a * b + c as the three-address v_fma_f64. The compiler lowers __builtin_fma with a register
 // addend that stays live (a loop-invariant polynomial coefficient) to v_mov_b64 + the two-address
 // v_fmac_f64, one extra issue per term; PP_FMA3=0 keeps __builtin_fma.
-#ifndef PP_FMA3
-#define PP_FMA3 1
-#endif
 __device__ __forceinline__ double fma3(double a, double b, double c) {
-#if PP_FMA3
     double r;
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-#else
-    return __builtin_fma(a, b, c);
-#endif
 }
 
 __device__ __forceinline__ int hiword(double x) { return (int)(__double_as_longlong(x) >> 32); }
@@ -355,13 +348,9 @@ __device__ __forceinline__ double div_rcp_nc(double n, double d, double r) {
 // the compiler's two-address v_fmac would need a copy of v first); 50 from an SGPR pair
 __device__ __forceinline__ double div50_nc(double v) {
     const double q0 = v * 0.02;
-#if PP_FMA3
     double e;
     asm("v_fma_f64 %0, -%1, %2, %3" : "=v"(e) : "v"(q0), "s"(50.0), "v"(v));
     return __builtin_fma(e, 0.02, q0);
-#else
-    return __builtin_fma(__builtin_fma(-q0, 50.0, v), 0.02, q0);
-#endif
 }
 
 // n / d with r ~ 1/d for a d known to lie in [2^-450, 2^450] (dok: sqrt_rd's fast path);

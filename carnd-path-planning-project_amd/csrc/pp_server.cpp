@@ -338,7 +338,7 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
                     const int nc = D.n_cars[i];
                     std::vector<int32_t> ids(nc);
                     for (int j = 0; j < nc; j++) ids[j] = D.car_id[(size_t)j * T + i];
-                    c.table.layout(ids.data(), nc, sl, i, TSl);
+                    c.table.layout(ids.data(), nc, sl, i, TSl, pp_debug_get(PP_DBG_POISON) == 1);
                 }
                 pp_result R;
                 memset(&R, 0, sizeof(R));

@@ -134,7 +134,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
            "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device",
-           "pp_num_lanes", "pp_libm_eval", "pp_set_prep_group"]
+           "pp_num_lanes", "pp_libm_eval", "pp_debug_set", "pp_debug_get"]
 
 
 def _load():
@@ -167,8 +167,10 @@ def _load():
                                   C.c_double, _dp, _dp, C.c_int32, _ip, _dp, _dp, _dp, _dp,
                                   C.c_int32, _ip, _dp, _dp, _ip]
     lib.pp_plan_frame.restype = C.c_int32
-    lib.pp_set_prep_group.argtypes = [C.c_int32]
-    lib.pp_set_prep_group.restype = C.c_int32
+    lib.pp_debug_set.argtypes = [C.c_int32, C.c_int32]
+    lib.pp_debug_set.restype = C.c_int32
+    lib.pp_debug_get.argtypes = [C.c_int32]
+    lib.pp_debug_get.restype = C.c_int32
     lib.pp_timing_enable.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
     lib.pp_timing_enable.restype = C.c_int32
     lib.pp_timing_read.argtypes = [C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int64)]
@@ -544,9 +546,40 @@ def plan_frame(m: Map, ego_x, ego_y, ego_yaw_deg, ego_speed_mph, prev_x, prev_y,
 DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
 
 
+# pp_debug_set keys and launch shapes (include/pp.h PP_DBG_*, PP_SHAPE_*)
+DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON = 0, 1, 2, 3
+SHAPE_AUTO, SHAPE_SPLIT, SHAPE_CAND_SMALL, SHAPE_STEP = 0, 1, 2, 3
+
+
+def debug_set(key, value):
+    """Process-wide debug switch of the library (pp_debug_set; 0 = the library's own choice)."""
+    _check(lib.pp_debug_set(key, value), "pp_debug_set")
+
+
+def debug_get(key):
+    return lib.pp_debug_get(key)
+
+
+class debug:
+    """Context manager: `with ppamd.debug(ppamd.DBG_SHAPE, ppamd.SHAPE_SPLIT): ...` sets a debug
+    switch and restores its previous value on exit."""
+
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+
+    def __enter__(self):
+        self.prev = debug_get(self.key)
+        debug_set(self.key, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        debug_set(self.key, self.prev)
+        return False
+
+
 def set_prep_group(lanes):
-    """K1 lanes per evaluation (1, 2, 4, 8, 16; 0 = automatic): pp_set_prep_group."""
-    _check(lib.pp_set_prep_group(lanes), "pp_set_prep_group")
+    """K1 lanes per evaluation (1, 2, 4, 8, 16; 0 = automatic): pp_debug_set(PP_DBG_PREP_GROUP)."""
+    debug_set(DBG_PREP_GROUP, lanes)
 
 
 def highway_map():

@@ -46,6 +46,7 @@ extern "C" {
 #define PP_ERR_HIP        -2   /* HIP runtime error                                            */
 #define PP_ERR_NOMEM      -3
 #define PP_ERR_NODEVICE   -4
+#define PP_ERR_STATE      -5   /* PP_DBG_POISON: a device buffer was not in its between-calls state */
 
 /* ---- per-scene status flags (pp_result.status) -------------------------------------------- */
 #define PP_ST_EGO_UNMATCHED  (1u << 0)  /* src/main.cpp:1302-1307 "can't lane match ego"        */
@@ -360,13 +361,32 @@ int32_t pp_serve(pp_map* m, const pp_server_opts* opts, volatile int32_t* stop, 
 /* RFC 6455 Sec-WebSocket-Accept for a client key (the handshake's known-answer check). */
 int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
 
+/* Debug switches (process-wide; tests and A/B measurements only). Every key defaults to 0, the
+ * library's own choice; results never depend on them (the tests check that bit for bit).
+ *   PP_DBG_PREP_GROUP  lanes per evaluation of the scene-preparation kernel K1: 1, 2, 4, 8, 16
+ *   PP_DBG_PREP_WAVES  K1's one-lane build: 3 or 4 waves per SIMD
+ *   PP_DBG_SHAPE       reference-mode launch shape: PP_SHAPE_SPLIT (k_prep, k_cand, k_emit),
+ *                      PP_SHAPE_CAND_SMALL (K1, then K2 + K4 in one launch), PP_SHAPE_STEP (the
+ *                      whole step in one launch, small batches)
+ *   PP_DBG_POISON      1: every call starts from NaN-filled intermediate buffers (prep workspace,
+ *                      winner record, staging copies, new car-table slots) and checks that the
+ *                      slow-group bitmap is all zero (PP_ERR_STATE otherwise), so no kernel can pass
+ *                      a test on what an earlier call left behind
+ * Returns PP_ERR_ARG for an unknown key or value. */
+#define PP_DBG_PREP_GROUP  0
+#define PP_DBG_PREP_WAVES  1
+#define PP_DBG_SHAPE       2
+#define PP_DBG_POISON      3
+#define PP_DBG_KEYS        4
+#define PP_SHAPE_SPLIT      1
+#define PP_SHAPE_CAND_SMALL 2
+#define PP_SHAPE_STEP       3
+int32_t pp_debug_set(int32_t key, int32_t value);
+int32_t pp_debug_get(int32_t key);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
  * (k_prep, k_cand, k_winner). pp_timing_read synchronises on the recorded events, returns the
  * summed milliseconds and launch counts per kernel, and clears the record. */
-/* Tuning: lanes per evaluation of the scene-preparation kernel (K1): 1, 2, 4, 8 or 16; 0 = automatic
- * (more lanes per scene when a batch is too small to fill the device). Results do not depend on it.
- * Process-wide; returns PP_ERR_ARG for other values. */
-int32_t pp_set_prep_group(int32_t lanes);
 int32_t pp_timing_enable(pp_map* m, int32_t device, int32_t enable);
 int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches3);
 

@@ -8,13 +8,16 @@ PKG = os.path.join(REPO, "carnd-path-planning-project_amd")
 for p in (PKG, os.path.join(REPO, "tests"), REPO):
     if p not in sys.path:
         sys.path.insert(0, p)
-# every pp_eval of the test run starts from a NaN-filled prep workspace and winner record, so no
-# kernel can pass a test on what an earlier call left there (csrc/pp_eval.hip, PP_POISON_WS)
-os.environ.setdefault("PP_POISON_WS", "1")
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    # every pp_eval of the test run starts from NaN-filled intermediates and outputs and checks
+    # that the slow-group bitmap is clear (include/pp.h PP_DBG_POISON), so no kernel can pass a
+    # test on what an earlier call left there; PP_TEST_NO_POISON=1 runs the suite without it
+    if os.environ.get("PP_TEST_NO_POISON") != "1":
+        import ppamd
+        ppamd.debug_set(ppamd.DBG_POISON, 1)
 
 
 def gpu_available():

@@ -1,0 +1,66 @@
+"""bench.py's roofline accounting (CPU): the PMC counters of a profiled launch are scaled to the
+measured launch per candidate, using the launch size the summary records, and every bench line
+names the BASELINE config it measures (a config-3 line divided a 262,144-scene launch's
+counters by the config-5 launch size)."""
+import json
+import os
+
+import pytest
+
+import bench
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PMC = json.load(open(os.path.join(REPO, "profiles", "pmc_summary.json")))
+
+
+def test_every_pmc_entry_states_its_launch():
+    for tag, e in PMC.items():
+        assert e["candidates_per_launch"] == e["scenes"] * e["candidates_per_scene"], tag
+        assert bench.pmc_tag(e["scenes"], e["candidates_per_scene"], e["n_points"], e["emit_paths"],
+                             e.get("draws", 1)) == tag
+
+
+@pytest.mark.parametrize("tag", [t for t in PMC if PMC[t]["emit_paths"]])
+def test_paths_traffic_covers_the_written_paths(tag):
+    """All-paths mode writes 16 B per point of every candidate: counted traffic below that is
+    impossible, at the profiled size and scaled to any other batch size of the same shape."""
+    e = PMC[tag]
+    C, N = e["candidates_per_scene"], e["n_points"]
+    for S in (e["scenes"], 4096, 1_000_003):
+        pmc = bench.pmc_for(PMC, S, C, N, True, 1)
+        assert pmc is e
+        bpc = bench.algorithmic_bytes_per_candidate(C, N, True)
+        traffic, pipe = bench.roofline_fields(pmc, S * C, bpc, 1.0)
+        written = 16.0 * N * C * S
+        assert traffic >= written, (S, traffic, written)
+        assert pipe >= traffic
+        # the algorithmic figure and the counters agree within the counted over-fetch (<= 1.3x)
+        assert traffic <= 1.3 * bpc * S * C
+
+
+def test_config5_entry_scales_to_shards():
+    e = PMC["k_cand_S2097152_C15_N50"]
+    pmc = bench.pmc_for(PMC, 262144, 15, 50, False, 1)      # an 8-GPU shard of config 5
+    assert pmc is e
+    t_full, _ = bench.roofline_fields(pmc, 2097152 * 15, 104.3, 1.0)
+    t_shard, _ = bench.roofline_fields(pmc, 262144 * 15, 104.3, 1.0)
+    assert t_full == pytest.approx(e["hbm_bytes_per_launch"])
+    assert t_shard == pytest.approx(t_full / 8)
+
+
+def test_unprofiled_shape_has_no_traffic_and_unsized_entry_fails():
+    assert bench.pmc_for(PMC, 4096, 9, 50, False, 1) is None
+    bad = {"k_cand_S10_C15_N50": {"candidates_per_scene": 15, "n_points": 50, "emit_paths": False,
+                                  "hbm_bytes_per_launch": 1.0, "source": "test"}}
+    with pytest.raises(ValueError):
+        bench.pmc_for(bad, 10, 15, 50, False, 1)
+
+
+def test_workload_names():
+    w = bench.workload_name
+    assert w(4096, 15, 5, 50, False, 1, 0) == "BASELINE config 2"
+    assert w(262144, 24, 8, 100, True, 1, 0) == "BASELINE config 3"
+    assert w(16384, 192, 1, 50, False, 64, 0) == "BASELINE config 4"
+    assert w(2097152, 15, 5, 50, False, 1, 0) == "BASELINE config 5"
+    assert w(262144, 15, 5, 50, False, 1, 0) == "BASELINE config 5"     # a shard of it
+    assert w(65536, 15, 5, 50, False, 1, 100).startswith("closed-loop")

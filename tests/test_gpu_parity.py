@@ -310,14 +310,14 @@ def test_prep_group_invariance(env, case):
 
 
 @pytest.mark.parametrize("case", ["random", "speed_edges"])
-def test_fused_small_invariance(env, case, monkeypatch):
-    """Reference mode without paths has three launch shapes: small batches run the whole step in
-    one launch (k_step_small: K1 with 16 lanes per scene, then K2 and K4 in the same block), or
-    with PP_STEP_FUSED=0 K1 then K2 + K4 in one launch (k_cand_small: the group's fast scenes, its
-    flagged scenes, then the block's team computes the recorded turns' sin/cos into the freed
-    spline slots and each winner lane replays its record); large batches (and PP_FUSED=0) run
-    k_prep, k_cand<false>, k_cand<true> and k_emit. All give bit-identical outputs and equal the
-    oracle. speed_edges: scenes flagged for the checked instantiation in most groups."""
+def test_fused_small_invariance(env, case):
+    """Reference mode without paths has three launch shapes (include/pp.h PP_DBG_SHAPE): small
+    batches run the whole step in one launch (k_step_small: K1 with 16 lanes per scene, then K2 and
+    K4 in the same block), or K1 then K2 + K4 in one launch (k_cand_small: the group's fast scenes,
+    its flagged scenes, then the block's team computes the recorded turns' sin/cos into the freed
+    spline slots and each winner lane replays its record); large batches run k_prep, k_cand<false>,
+    k_cand<true> and k_emit. All give bit-identical outputs and equal the oracle. speed_edges:
+    scenes flagged for the checked instantiation in most groups."""
     S = 1200
     sc = ppamd.synth_host(env["m"], S, seed=515, first=99)
     if case == "speed_edges":
@@ -328,10 +328,10 @@ def test_fused_small_invariance(env, case, monkeypatch):
     d = to_dev(env, sc)
     prm = ppamd.default_params()
     outs = {}
-    for name, f, st in (("k_emit", "0", "0"), ("k_cand_small", "1", "0"), ("step", "1", "1")):
-        monkeypatch.setenv("PP_FUSED", f)
-        monkeypatch.setenv("PP_STEP_FUSED", st)
-        outs[name] = run_gpu(env, d, prm, info=True)
+    for name, shape in (("k_emit", ppamd.SHAPE_SPLIT), ("k_cand_small", ppamd.SHAPE_CAND_SMALL),
+                        ("step", ppamd.SHAPE_STEP)):
+        with ppamd.debug(ppamd.DBG_SHAPE, shape):
+            outs[name] = run_gpu(env, d, prm, info=True)
     def same(a, b):
         if a.dtype.names:
             return all(same(a[f], b[f]) for f in a.dtype.names)
@@ -339,19 +339,17 @@ def test_fused_small_invariance(env, case, monkeypatch):
     for name in ("k_cand_small", "step"):
         for k, v in outs["k_emit"].items():
             assert same(outs[name][k], v), (name, k)
-    outs["fused"] = outs["step"]
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
-    compare(outs["fused"], ref)
+    compare(outs["step"], ref)
 
 
 @pytest.mark.parametrize("case", ["random", "ties_ids", "draws"])
-def test_prep_staged_invariance(env, case, monkeypatch):
-    """K1 on large batches stages every car's x, y in LDS (k_prep_st: coalesced row-order loads,
-    matching nearest first from LDS, planner pass in row order); PP_PREP_ST=0 forces the gathering
-    k_prep, and PP_PREP_W4=1 its 4-waves-per-SIMD build (picked for 262,144-scene shards). All give
-    bit-identical outputs (scene info included) and equal the oracle. Cases:
-    random scenes; tied duplicate cars with -1, negative and large ids; Monte-Carlo draws (the
-    position noise applied where x, y are staged, the velocity noise in the row-order pass)."""
+def test_prep_waves_invariance(env, case):
+    """K1's one-lane-per-evaluation kernel has a 3- and a 4-waves-per-SIMD build (the 4-wave one is
+    picked where a batch's waves fill whole rounds of 4 better, e.g. 262,144-scene shards;
+    PP_DBG_PREP_WAVES forces either). Both give bit-identical outputs (scene info included) and
+    equal the oracle. Cases: random scenes; tied duplicate cars with -1, negative and large ids;
+    Monte-Carlo draws."""
     S = 1500
     sc = ppamd.synth_host(env["m"], S, seed=4711, first=123)
     kw = {"emit_paths": True}
@@ -366,23 +364,17 @@ def test_prep_staged_invariance(env, case, monkeypatch):
     prm = ppamd.default_params(**kw)
     d = to_dev(env, sc)
     outs = {}
-    try:
-        ppamd.set_prep_group(1)          # one lane per evaluation at this size too
-        # "0": the gathering k_prep (3 waves/SIMD); "1": k_prep_st; "w4": k_prep's 4-wave build
-        for name, st, w4 in (("0", "0", "0"), ("1", "1", "0"), ("w4", "0", "1")):
-            monkeypatch.setenv("PP_PREP_ST", st)
-            monkeypatch.setenv("PP_PREP_W4", w4)
-            outs[name] = run_gpu(env, d, prm, info=case != "draws")
-    finally:
-        ppamd.set_prep_group(0)
+    with ppamd.debug(ppamd.DBG_PREP_GROUP, 1):          # one lane per evaluation at this size too
+        for w in (3, 4):
+            with ppamd.debug(ppamd.DBG_PREP_WAVES, w):
+                outs[w] = run_gpu(env, d, prm, info=case != "draws")
 
     def same(a, b):
         if a.dtype.names:
             return all(same(a[f], b[f]) for f in a.dtype.names)
         return np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
-    for name in ("1", "w4"):
-        for k, v in outs["0"].items():
-            assert same(outs[name][k], v), (name, k)
+    for k, v in outs[3].items():
+        assert same(outs[4][k], v), k
     if case != "draws":
         ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
-        compare(outs["1"], ref)
+        compare(outs[3], ref)

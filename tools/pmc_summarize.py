@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -23,9 +24,26 @@ for k, d in vals.items():
     # rocprofv3 reports one row per dispatch per counter (already summed over XCDs/SEs)
     summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
 print(json.dumps(summary, indent=1))
+
+
+def parse_tag(tag):
+    """Launch shape from a bench tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>]."""
+    m = re.match(r"k_cand_S(\d+)_C(\d+)_N(\d+)(_paths)?(?:_D(\d+))?$", tag)
+    if not m:
+        raise SystemExit(f"pmc_summarize: tag {tag!r} is not k_cand_S<S>_C<C>_N<N>[_paths][_D<D>]")
+    S, C, N = int(m.group(1)), int(m.group(2)), int(m.group(3))
+    return {"scenes": S, "candidates_per_scene": C, "n_points": N, "emit_paths": bool(m.group(4)),
+            "draws": int(m.group(5) or 1), "candidates_per_launch": S * C}
+
+
+# the dominant kernel of a step: k_cand (both instantiations); the small-batch shapes fuse it
+# into k_cand_small / k_step_small
+DOMINANT = ("k_cand<", "k_cand_small", "k_step_small")
+STEP_KERNELS = ("k_prep", "k_prep_g2", "k_prep_g4", "k_prep_g8", "k_prep_g16", "k_cand", "k_cand_small",
+                "k_step_small", "k_emit", "k_winner")
 if tag:
-    # k_cand is launched as the fast and the slow-heading instantiation; traffic = their sum
-    parts = [v for k, v in summary.items() if k.startswith("k_cand")]
+    shape = parse_tag(tag)
+    parts = [v for k, v in summary.items() if k.startswith(DOMINANT)]
     kc = {c: sum(p.get(c, 0.0) for p in parts) for c in set().union(*parts)} if parts else {}
     out = {}
     p = "profiles/pmc_summary.json"
@@ -34,16 +52,16 @@ if tag:
     fetch = kc.get("FETCH_SIZE")
     write = kc.get("WRITE_SIZE")
     if fetch is not None and write is not None:
-        # every kernel of one evaluation (k_prep, both k_cand instantiations, k_emit / k_winner):
-        # the step's whole HBM traffic, beside k_cand's own
+        # every kernel of one evaluation: the step's whole HBM traffic, beside the dominant kernel's
         per_kernel = {k: (2 * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)) * 1024.0
-                      for k, v in summary.items()
-                      if k.split("<")[0] in ("k_prep", "k_cand", "k_emit", "k_winner")}
-        out[tag] = {"hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
-                    "pipeline_bytes_per_step": sum(per_kernel.values()),
-                    "pipeline_bytes_by_kernel": per_kernel,
-                    "fetch_kib_raw": fetch, "write_kib": write,
-                    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), k_cand instantiations summed",
-                    "counters": kc}
+                      for k, v in summary.items() if k.split("<")[0] in STEP_KERNELS}
+        out[tag] = dict(shape, **{
+            "kernels": sorted(k for k in summary if k.startswith(DOMINANT)),
+            "hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
+            "pipeline_bytes_per_step": sum(per_kernel.values()),
+            "pipeline_bytes_by_kernel": per_kernel,
+            "fetch_kib_raw": fetch, "write_kib": write,
+            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), dominant-kernel instantiations summed",
+            "counters": kc})
         json.dump(out, open(p, "w"), indent=1)
         print("wrote", p, tag)
