@@ -109,6 +109,81 @@ __device__ __forceinline__ void st_xy(double* p, double x, double y) {
     const dv2 xy = {x, y};
     __builtin_nontemporal_store(xy, (dv2*)p);
 }
+// ---- The output frame: the local -> global transform of TrajectoryBuilder::build (src/main.cpp:
+// 786-823, 994-1007, 1033-1037). It only maps points out (no decision of the loop reads it), so it
+// is evaluated in fused multiply-adds; every launch shape that writes points (k_cand emit_paths,
+// k_emit, the fused small-batch kernels, k_winner) calls these same functions, so their outputs
+// stay bit-identical to each other (and within ~1e-12 m of the reference's unfused sequence).
+struct OutFrame { double cx, cy, ca, sa; };   // centre, cos and sin of the frame's heading
+__device__ __forceinline__ void frame_pt(const OutFrame& f, double px, double py, double& ox, double& oy) {
+    ox = __builtin_fma(px, f.ca, -(py * f.sa)) + f.cx;
+    oy = __builtin_fma(px, f.sa, py * f.ca) + f.cy;
+}
+// the turn of a curvature adjustment (src/main.cpp:986-997) at local point (px, py): the centre
+// rotates about the current output point, the heading's (cos, sin) by the angle-sum rotation
+__device__ __forceinline__ void frame_turn(OutFrame& f, double px, double py, double cr, double sr) {
+    double tx, ty;
+    frame_pt(f, px, py, tx, ty);
+    const double vx = f.cx - tx, vy = f.cy - ty;
+    f.cx = tx + __builtin_fma(vx, cr, -(vy * sr));
+    f.cy = ty + __builtin_fma(vx, sr, vy * cr);
+    const double nca = __builtin_fma(f.ca, cr, -(f.sa * sr)), nsa = __builtin_fma(f.sa, cr, f.ca * sr);
+    f.ca = nca;
+    f.sa = nsa;
+}
+// the turn angle rot = nad - adiff (src/main.cpp:978-986), nad = +-nc / speed / 50 with the sign of
+// adiff: k_cand<false> (speed +0 or in [2^-113, 2^21]) by a reciprocal, the checked instantiation by
+// IEEE divisions (speed 0: +-inf or NaN, which turns the rest of the path into NaN either way)
+template <bool kLarge>
+__device__ __forceinline__ double turn_angle(double nc, double speed, double adiff) {
+    double nad = kLarge ? nc / speed / 50 : (nc * 0.02) * ppm::rcp_nr(speed);
+    if (adiff < 0) nad *= -1;
+    return nad - adiff;
+}
+// sin and cos of a turn: fdlibm's kernel polynomials in fused form (~1 ulp) on [-pi/4, pi/4]; a
+// wider turn (rare: a wide step turn, or a step slower than ~0.7 m/s) is first reduced by the
+// nearest multiple of pi/2 (two-part Cody-Waite: |error| < 1e-15 rad up to kMediumMax, plenty for an
+// output frame) and its quadrant applied after; beyond kMediumMax (only from an absurd telemetry
+// heading, in the checked instantiation) the library's reduction
+// a constant materialised at its use (scalar moves) rather than hoisted out of the step loop into
+// registers that the loop then holds throughout
+__device__ __forceinline__ double kc(double v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+template <bool kLarge>
+__device__ __forceinline__ void turn_sincos(double r, double& s, double& c) {
+    double y = r;
+    int q = 0;
+    if (__builtin_expect(!(fabs(r) <= 0.78539816339744828), 0)) {
+        if (kLarge && !(fabs(r) <= ppm::kMediumMax)) {
+            ppm::sincos_pp<true>(r, s, c);
+            return;
+        }
+        const double k = __builtin_rint(r * 6.36619772367581382433e-01);
+        y = __builtin_fma(-k, kc(1.57079632673412561417e+00), r);
+        y = __builtin_fma(-k, kc(6.07710050650619224932e-11), y);
+        q = (int)k;
+    }
+    const double z = y * y;
+    double ps = __builtin_fma(z, kc(1.58969099521155010221e-10), kc(-2.50507602534068634195e-08));
+    ps = __builtin_fma(z, ps, kc(2.75573137070700676789e-06));
+    ps = __builtin_fma(z, ps, kc(-1.98412698298579493134e-04));
+    ps = __builtin_fma(z, ps, kc(8.33333333332248946124e-03));
+    ps = __builtin_fma(z, ps, kc(-1.66666666666666324348e-01));
+    double pc = __builtin_fma(z, kc(-1.13596475577881948265e-11), kc(2.08757232129817482790e-09));
+    pc = __builtin_fma(z, pc, kc(-2.75573143513906633035e-07));
+    pc = __builtin_fma(z, pc, kc(2.48015872894767294178e-05));
+    pc = __builtin_fma(z, pc, kc(-1.38888888888741095749e-03));
+    pc = __builtin_fma(z, pc, kc(4.16666666666666019037e-02));
+    s = __builtin_fma(y * z, ps, y);
+    c = __builtin_fma(z * z, pc, __builtin_fma(-0.5, z, 1.0));
+    if (__builtin_expect(q != 0, 0)) {
+        if (q & 1) { const double t = s; s = c; c = -t; }
+        if (q & 2) { s = -s; c = -c; }
+    }
+}
+
 // Tuning constants (each measured against its alternatives):
 constexpr int kEmitChunk = 4;      // k_emit: recorded steps loaded together per lane (large batches)
 constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
@@ -1109,7 +1184,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     if (mflags & kMetaTrunc) R.flags |= PP_ST_SPLINE_TRUNC;
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
     double pos_x = 0, pos_y = 0;
-    double ca = ca0, sa = sa0;
+    OutFrame F = {cx, cy, ca0, sa0};
     (void)angle;      // the frame turns by rotating (ca, sa) (src/main.cpp:996-997)
     double cur_t = 0.02;
     int ng = 0;
@@ -1139,10 +1214,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             pos_x += cc_ * dstep;
             pos_y += sc_ * dstep;
             if (kOutMode != 0 && kOut) {
-                const double tx = pos_x * ca - pos_y * sa;
-                const double ty = pos_x * sa + pos_y * ca;
-                if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
-                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, tx + cx, ty + cy);
+                double ox, oy;
+                frame_pt(F, pos_x, pos_y, ox, oy);
+                if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = ox; wy[ng * ws] = oy; }
+                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3)) st_xy(px + ng * ps, ox, oy);
             }
             if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
             ng++;
@@ -1262,39 +1337,16 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 double nc = P.maximum_acc - acc;
                 if (nc < 0) nc = 0;
                 if (kOutMode != 0 && kOut) {
-                    // the transform's turn about the current point (src/main.cpp:986-997); the frame's
-                    // new cos/sin by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead
-                    // of sin/cos of the accumulated angle (~1 ulp per adjustment, as k_emit; DESIGN.md
-                    // §5); rot by reciprocal divisions in k_cand<false> (as the recorded rot, below)
-                    double nad = kLarge ? nc / speed / 50
-                                        : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
-                    if (adiff < 0) nad *= -1;
-                    const double rot = nad - adiff;
-                    double tpx = pos_x * ca - pos_y * sa;
-                    double tpy = pos_x * sa + pos_y * ca;
-                    tpx = tpx + cx;
-                    tpy = tpy + cy;
-                    const double vx = cx - tpx, vy = cy - tpy;
+                    // the output frame turns about the current point (src/main.cpp:986-997)
                     double cr, sr;
-                    ppm::sincos_pp<kLarge>(rot, sr, cr);
-                    const double rvx = vx * cr - vy * sr;
-                    const double rvy = vx * sr + vy * cr;
-                    cx = tpx + rvx;
-                    cy = tpy + rvy;
-                    const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
-                    ca = nca; sa = nsa;
+                    turn_sincos<kLarge>(turn_angle<kLarge>(nc, speed, adiff), sr, cr);
+                    frame_turn(F, pos_x, pos_y, cr, sr);
                 }
                 if (kOutMode == 3 && kRec) {
-                    // rot only turns the output transform (k_emit), so it need not carry the
-                    // IEEE quotients' last bit: k_cand<false> divides by reciprocals (speed is +0
-                    // or in [2^-113, 2^21], nc in [0, maximum_acc]; speed 0 gives a NaN rot where
-                    // the IEEE quotient gives +-inf: both turn the rest of the path into NaN)
-                    double nad = kLarge ? nc / speed / 50
-                                        : ppm::div_rcp_nc(ppm::div_rcp_nc(nc, speed, ppm::rcp_nr(speed)), 50.0, 0.02);
-                    if (adiff < 0) nad *= -1;
+                    // the turn angle for k_emit's replay of the output frame
                     double* rp = rec_rot(rec - rs, rstride, ng, ws, rs);
                     if (PP_CHKP(rp, rec, nrec, 6))
-                        PP_ST(rp, nad - adiff);   // rot (src/main.cpp:986)
+                        PP_ST(rp, turn_angle<kLarge>(nc, speed, adiff));   // rot (src/main.cpp:986)
                     const uint64_t bit = 1ull << (ng & 63);
                     if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
                 }
@@ -1320,11 +1372,11 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         arg += sp_step;
         pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
         if (kOutMode != 0 && kOut) {
-            const double tx = pos_x * ca - pos_y * sa;
-            const double ty = pos_x * sa + pos_y * ca;
-            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = tx + cx; wy[ng * ws] = ty + cy; }
+            double ox, oy;
+            frame_pt(F, pos_x, pos_y, ox, oy);
+            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = ox; wy[ng * ws] = oy; }
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
-                st_xy(px + ng * ps, tx + cx, ty + cy);      // one 16-B store (x, y)
+                st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
         }
         if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
         ng++;
@@ -1391,8 +1443,7 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
         for (int i = 0; i < PP_PREV_KEEP; i++)
             if (i < K) { PP_ST(out.next_x + (int64_t)i * S + s, kx[i]); PP_ST(out.next_y + (int64_t)i * S + s, ky[i]); }
     }
-    double cx = pv.pos_x[s], cy = pv.pos_y[s];
-    double ca = pv.ca_p[s], sa = pv.sa_p[s];
+    OutFrame F = {pv.pos_x[s], pv.pos_y[s], pv.ca_p[s], pv.sa_p[s]};
     double pxp = 0, pyp = 0;                       // local position before the step
     for (int g0 = 0; g0 < ng; g0 += kChunk) {
         double px_[kChunk], py_[kChunk];
@@ -1409,21 +1460,12 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
         for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
             if (g >= ng) break;
-            if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
-                const double cr = pcr[g], sr = psr[g];
-                const double tpx = (pxp * ca - pyp * sa) + cx;
-                const double tpy = (pxp * sa + pyp * ca) + cy;
-                const double vx = cx - tpx, vy = cy - tpy;
-                cx = tpx + (vx * cr - vy * sr);
-                cy = tpy + (vx * sr + vy * cr);
-                const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
-                ca = nca; sa = nsa;
-            }
-            const double tx = px_[u] * ca - py_[u] * sa;
-            const double ty = px_[u] * sa + py_[u] * ca;
+            if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) frame_turn(F, pxp, pyp, pcr[g], psr[g]);
+            double ox, oy;
+            frame_pt(F, px_[u], py_[u], ox, oy);
             if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
-            PP_ST(out.next_x + (int64_t)(K + g) * S + s, tx + cx);
-            PP_ST(out.next_y + (int64_t)(K + g) * S + s, ty + cy);
+            PP_ST(out.next_x + (int64_t)(K + g) * S + s, ox);
+            PP_ST(out.next_y + (int64_t)(K + g) * S + s, oy);
             pxp = px_[u];
             pyp = py_[u];
         }
@@ -1648,8 +1690,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             if (!PP_CHKP(rr, rec, nrec, 18)) continue;
             const double rt = *rr;
             double sr, cr;
-            if (fabs(rt) <= ppm::kMediumMax) ppm::sincos_pp<false>(rt, sr, cr);
-            else ppm::sincos_pp<true>(rt, sr, cr);
+            turn_sincos<true>(rt, sr, cr);
             pcr[idx] = cr; psr[idx] = sr;
         }
         __syncthreads();
@@ -1774,36 +1815,21 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         for (int i = 0; i < PP_PREV_KEEP; i++)
             if (i < K) { PP_ST(out.next_x + (int64_t)i * S + s, kx[i]); PP_ST(out.next_y + (int64_t)i * S + s, ky[i]); }
     }
-    double cx = pv.pos_x[s], cy = pv.pos_y[s], tangle = pv.angle[s];
-    double ca = pv.ca_p[s], sa = pv.sa_p[s];
+    OutFrame F = {pv.pos_x[s], pv.pos_y[s], pv.ca_p[s], pv.sa_p[s]};
     const uint64_t m0 = adjm[s], m1 = adjm[S + s];
     double pxp = 0, pyp = 0;                       // local position before the step
-    // The adjusted steps are sparse and scattered over the wave's lanes, so the rotation block
-    // runs, with few lanes active, on most steps: it is kept short. The heading's sin/cos follow
-    // by the angle-sum rotation of (ca, sa) by (cos rot, sin rot) instead of sin/cos of the
-    // accumulated angle (src/main.cpp:996-997): equal to ~1 ulp per adjustment.
-    // Steps are taken kEmitChunk at a time with all of the chunk's record loads (the rotation
-    // only where the step's bit is set) in flight together: one memory round trip per chunk
-    // instead of one or two per step.
-    // A rotation beyond sincos_pp's medium range (a step that slowed to ~1e-7 m/s) sends the
-    // lane's chunk through a per-step loop with the library reduction, re-reading the record:
-    // the unrolled chunk then holds no call and stays register-light.
-    constexpr int kEmitChunk = kChunk;
-    auto rotate = [&](double rot, double& cr, double& sr) {
-        const double tpx = (pxp * ca - pyp * sa) + cx;
-        const double tpy = (pxp * sa + pyp * ca) + cy;
-        const double vx = cx - tpx, vy = cy - tpy;
-        cx = tpx + (vx * cr - vy * sr);
-        cy = tpy + (vx * sr + vy * cr);
-        const double nca = ca * cr - sa * sr, nsa = sa * cr + ca * sr;
-        ca = nca; sa = nsa;
-        (void)rot;
-    };
-    for (int g0 = 0; g0 < ng; g0 += kEmitChunk) {
-        double px_[kEmitChunk], py_[kEmitChunk], rt[kEmitChunk];
+    // The adjusted steps are sparse and scattered over the wave's lanes, so the turn block runs,
+    // with few lanes active, on most steps: it is kept short (frame_turn, turn_sincos). Steps are
+    // taken kChunk at a time with all of the chunk's record loads (the turn angle only where the
+    // step's bit is set) in flight together: one memory round trip per chunk instead of one or two
+    // per step. A turn beyond sincos_pp's medium range (a step that slowed to ~1e-7 m/s) sends the
+    // lane's chunk through a per-step loop with the library reduction, re-reading the record: the
+    // unrolled chunk then holds no call and stays register-light.
+    for (int g0 = 0; g0 < ng; g0 += kChunk) {
+        double px_[kChunk], py_[kChunk], rt[kChunk];
         uint32_t bits = 0;
 #pragma unroll
-        for (int u = 0; u < kEmitChunk; u++) {
+        for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
             const bool bit = g < ng && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
             bits |= bit ? 1u << u : 0u;
@@ -1817,19 +1843,19 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         }
         bool huge = false;
 #pragma unroll
-        for (int u = 0; u < kEmitChunk; u++) huge |= !(fabs(rt[u]) <= ppm::kMediumMax);
+        for (int u = 0; u < kChunk; u++) huge |= !(fabs(rt[u]) <= ppm::kMediumMax);
         if (__builtin_expect(huge, 0)) {
-            for (int g = g0; g < ng && g < g0 + kEmitChunk; g++) {
+            for (int g = g0; g < ng && g < g0 + kChunk; g++) {
                 if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
-                    const double rot = *rec_rot(rec, rstride, g, S, s);
                     double cr, sr;
-                    ppm::sincos_pp<true>(rot, sr, cr);
-                    rotate(rot, cr, sr);
+                    turn_sincos<true>(*rec_rot(rec, rstride, g, S, s), sr, cr);
+                    frame_turn(F, pxp, pyp, cr, sr);
                 }
-                double qx, qy;
+                double qx, qy, ox, oy;
                 rec_ld(rec, rstride, g, S, s, qx, qy);
-                out.next_x[(int64_t)(K + g) * S + s] = (qx * ca - qy * sa) + cx;
-                out.next_y[(int64_t)(K + g) * S + s] = (qx * sa + qy * ca) + cy;
+                frame_pt(F, qx, qy, ox, oy);
+                out.next_x[(int64_t)(K + g) * S + s] = ox;
+                out.next_y[(int64_t)(K + g) * S + s] = oy;
                 pxp = qx;
                 pyp = qy;
             }
@@ -1837,26 +1863,25 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
         }
         // sin/cos of the chunk's turns first (rt = 0 where no turn): independent of each other and
         // of the chain of turns below, so they overlap instead of queueing behind it
-        double crs[kEmitChunk], srs[kEmitChunk];
+        double crs[kChunk], srs[kChunk];
         if (bits) {
 #pragma unroll
-            for (int u = 0; u < kEmitChunk; u++) ppm::sincos_pp<false>(rt[u], srs[u], crs[u]);
+            for (int u = 0; u < kChunk; u++) turn_sincos<false>(rt[u], srs[u], crs[u]);
         }
 #pragma unroll
-        for (int u = 0; u < kEmitChunk; u++) {
+        for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
             if (g >= ng) break;
-            if ((bits >> u) & 1) rotate(rt[u], crs[u], srs[u]);
-            const double tx = px_[u] * ca - py_[u] * sa;
-            const double ty = px_[u] * sa + py_[u] * ca;
+            if ((bits >> u) & 1) frame_turn(F, pxp, pyp, crs[u], srs[u]);
+            double ox, oy;
+            frame_pt(F, px_[u], py_[u], ox, oy);
             if (!PP_CHKP(out.next_x + (int64_t)(K + g) * S + s, nx, nnext, 17)) break;
-            PP_ST(out.next_x + (int64_t)(K + g) * S + s, tx + cx);
-            PP_ST(out.next_y + (int64_t)(K + g) * S + s, ty + cy);
+            PP_ST(out.next_x + (int64_t)(K + g) * S + s, ox);
+            PP_ST(out.next_y + (int64_t)(K + g) * S + s, oy);
             pxp = px_[u];
             pyp = py_[u];
         }
     }
-    (void)tangle;
     for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
 }
 

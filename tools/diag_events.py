@@ -19,14 +19,22 @@ NAMES = ["step", "seg_reload", "ramp_div", "wide_turn", "limiter", "override", "
 
 
 def main():
+    import argparse
     import torch
     import ppamd
-    S = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scenes", type=int, default=262144)
+    ap.add_argument("--n-speeds", type=int, default=5)
+    ap.add_argument("--n-points", type=int, default=50)
+    ap.add_argument("--emit-paths", action="store_true")
+    a = ap.parse_args()
+    S = a.scenes
     lib = C.CDLL(ppamd.LIB_PATH)
     lib.pp_diag_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int32]
     wx, wy = ppamd.highway_map()
     m = ppamd.Map(wx, wy)
-    prm = ppamd.default_params(n_speeds=5)
+    prm = ppamd.default_params(n_speeds=a.n_speeds, n_points=a.n_points, emit_paths=a.emit_paths,
+                               speed_offsets=[-6, -4, -3, -2, -1, 0, 2] if a.n_speeds == 8 else None)
     scenes = ppamd.synth_device(m, S, seed=0x5EED0001, device=0)
     res = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
     buf = (C.c_ulonglong * 64)()
@@ -35,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     assert lib.pp_diag_read(buf, 1) == 0
     lanes0, waves0 = buf[0], buf[1]
-    out = {"scenes": S, "lane_steps": lanes0, "wave_steps": waves0,
+    out = {"scenes": S, "n_speeds": a.n_speeds, "n_points": a.n_points, "emit_paths": a.emit_paths, "lane_steps": lanes0, "wave_steps": waves0,
            "lanes_per_wave_step": lanes0 / max(waves0, 1)}
     for k, n in enumerate(NAMES):
         if not n or k == 0:
