@@ -2373,11 +2373,23 @@ int prep_group(int64_t Sv) {
     return G;
 }
 
+// Scenes per k_cand group (C <= 256): at most 256 / C (one 256-lane block) and 64 / NL (spline
+// slots: phase A's serial steps run on one wave), chosen so the block's waves carry the fewest
+// idle lanes through phase B (largest such count on ties): C = 15 -> 17 scenes (255 of 256
+// lanes), C = 24 (config 3) -> 8 scenes in exactly 3 waves instead of 10 in 4 waves with 16 idle
+// lanes.
 int cands_per_block(int C) {
-    int spb = 256 / C;
-    if (spb > 64 / NL) spb = 64 / NL;      // <= 64 LDS spline slots per workgroup
-    if (spb < 1) spb = 1;
-    return spb;
+    int hi = 256 / C;
+    if (hi > 64 / NL) hi = 64 / NL;
+    if (hi < 1) return 1;
+    int best = hi;
+    double bu = 0;
+    for (int spb = hi; spb >= 1; spb--) {
+        const int t = spb * C;
+        const double u = (double)t / (double)(((t + 63) / 64) * 64);
+        if (u > bu + 1e-9) { bu = u; best = spb; }
+    }
+    return best;
 }
 
 // callers hold M->mu; `st` is the stream the workspace belongs to
