@@ -7,11 +7,15 @@ simulator shim (csrc/pp_wsproto.h), the car table (csrc/pp_cartable.h) and the o
 The driver runs the codec corpus of tests/test_codec.py (simulator-style frames, special number
 spellings, non-telemetry and malformed frames) plus seeded mutations of every frame, seeded
 WebSocket streams with corrupted frames, random car tables and random scenes through the oracle.
-Any sanitizer report aborts it; the test requires a clean exit. CPU only."""
+Any sanitizer report aborts it; the test requires a clean exit. The second test runs the CPU tests
+of the codec, the number formats, the server protocol and the car table against the product
+library built with its host code under ASan + UBSan (`make sanitize-lib`: ppamd/libppamd_asan.so,
+clang's runtimes, loaded by LD_PRELOAD). CPU only."""
 import os
 import shutil
 import struct
 import subprocess
+import sys
 
 import pytest
 
@@ -51,3 +55,29 @@ def test_host_code_sanitizer_clean(driver, tmp_path):
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
     assert r.stdout.strip().endswith("clean")
     assert "codec: 120 corpus frames, 18000 mutants" in r.stdout
+
+
+def test_python_cpu_tests_against_sanitized_library():
+    lib = os.path.join(PKG, "ppamd", "libppamd_asan.so")
+    r = subprocess.run(["make", "-C", PKG, "-s", "sanitize-lib"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rt = subprocess.run(["/opt/rocm/lib/llvm/bin/clang++", "-print-file-name=libclang_rt.asan-x86_64.so"],
+                        capture_output=True, text=True).stdout.strip()
+    if not os.path.isabs(rt) or not os.path.exists(rt):
+        import glob
+        found = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
+        assert found, "clang ASan runtime not found"
+        rt = found[0]
+    env = dict(os.environ, PPAMD_LIB=lib, LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", PP_TEST_NO_POISON="1")
+    tests = [os.path.join(REPO, "tests", t) for t in
+             ("test_codec.py", "test_numfmt.py", "test_server.py", "test_cartable.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-m", "not gpu", "-p", "no:cacheprovider", *tests,
+                        "-k", "not sanitize"], capture_output=True, text=True, timeout=900, env=env, cwd=REPO)
+    print(r.stdout[-2000:])
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-4000:]
+    # the sanitized library is the one that was loaded (it cannot load without the preloaded runtime)
+    chk = subprocess.run([sys.executable, "-c", "import ppamd; print(ppamd.LIB_PATH)"], capture_output=True,
+                         text=True, env=dict(env, PYTHONPATH=PKG), cwd=REPO)
+    assert chk.stdout.strip() == lib, chk.stdout + chk.stderr
