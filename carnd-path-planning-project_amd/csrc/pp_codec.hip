@@ -2,9 +2,11 @@
 // pp_control_format_device). The same parser and writer as the host codec (pp_jsonparse.h,
 // pp_numfmt.h) instantiated for the device: one lane per frame, bytes read through a 16-byte
 // register window (one global_load_dwordx4 per 16 bytes of the frame), control text assembled in
-// a 16-byte register and stored as aligned dwordx4 into a per-frame slot. A frame or message
-// that needs libc (a number outside the exact conversions' domain, more than kDevRows
-// sensor_fusion rows, a slot overflow) is flagged for the host instead: status PP_MSG_HOST / len -1.
+// a 16-byte register and stored as aligned dwordx4 into a per-frame slot. The first kDevRows
+// sensor_fusion rows are held in registers; a frame with more moves them into its output columns
+// and takes the rest there (ordered in place, std::map order). A frame or message that needs libc
+// (a number outside the exact conversions' domain, more rows than the batch's car columns, a slot
+// overflow) is flagged for the host instead: status PP_MSG_HOST / len -1.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,6 +40,11 @@ struct DevSink {
     bool host;
     int id[kDevRows];
     double cx[kDevRows], cy[kDevRows], cvx[kDevRows], cvy[kDevRows];
+    // the frame's output columns (row j at [j * S + s]), used once it has more than kDevRows rows
+    int32_t* oid;
+    double *ox, *oy, *ovx, *ovy;
+    int64_t S;
+    int stride;
     __device__ void scalar(int f, double v) {
         if (f == 0) x = v; else if (f == 1) y = v; else if (f == 2) yaw = v; else speed = v;
     }
@@ -46,8 +53,19 @@ struct DevSink {
     }
     __device__ void prev_count(int which, int k) { if (which) npy = k; else npx = k; }
     __device__ void row(int i, double a, double b, double c, double d) {
-        if (n >= kDevRows) { host = true; return; }
-        id[n] = i; cx[n] = a; cy[n] = b; cvx[n] = c; cvy[n] = d;
+        if (n < kDevRows) {
+            id[n] = i; cx[n] = a; cy[n] = b; cvx[n] = c; cvy[n] = d;
+        } else if (n < stride) {
+            if (n == kDevRows) {                       // move the register rows into the columns
+#pragma unroll
+                for (int j = 0; j < kDevRows; j++) {
+                    oid[j * S] = id[j]; ox[j * S] = cx[j]; oy[j * S] = cy[j]; ovx[j * S] = cvx[j]; ovy[j * S] = cvy[j];
+                }
+            }
+            oid[n * S] = i; ox[n * S] = a; oy[n * S] = b; ovx[n * S] = c; ovy[n * S] = d;
+        } else {
+            host = true;                               // more rows than the batch has columns
+        }
         n++;
     }
     __device__ bool host_needed() const { return host; }
@@ -70,6 +88,10 @@ __global__ __launch_bounds__(256) void k_tel_parse(const uint4* buf, const int64
     K.n = 0;
     K.host = false;
     K.x = K.y = K.yaw = K.speed = 0;
+    K.oid = (int32_t*)out.car_id + s; K.ox = (double*)out.car_x + s; K.oy = (double*)out.car_y + s;
+    K.ovx = (double*)out.car_vx + s; K.ovy = (double*)out.car_vy + s;
+    K.S = S;
+    K.stride = stride;
     const int64_t o0 = off[s], o1 = off[s + 1];
     int st = ppjson::kMsgBad;
     if (o1 >= o0) {
@@ -79,8 +101,10 @@ __global__ __launch_bounds__(256) void k_tel_parse(const uint4* buf, const int64
         if (st == ppjson::kMsgOk && K.npx != K.npy) st = ppjson::kMsgBad;
     }
     int u = 0;
+    const bool cols = K.n > kDevRows;                  // the rows are in the output columns
     if (st == ppjson::kMsgOk) {
-        u = ppjson::map_order(K.id, K.cx, K.cy, K.cvx, K.cvy, K.n);
+        u = cols ? ppjson::map_order(K.oid, K.ox, K.oy, K.ovx, K.ovy, K.n, S)
+                 : ppjson::map_order(K.id, K.cx, K.cy, K.cvx, K.cvy, K.n);
         if (u > stride) st = ppjson::kMsgTooManyCars;
     }
     const bool ok = st == ppjson::kMsgOk || st == ppjson::kMsgTooManyCars;
@@ -100,6 +124,7 @@ __global__ __launch_bounds__(256) void k_tel_parse(const uint4* buf, const int64
     for (int j = 0; j < stride; j++) {
         const int64_t ix = (int64_t)j * S + s;
         const bool on = j < nc;
+        if (cols && on) continue;                      // already in place
         ((int32_t*)out.car_id)[ix] = on ? K.id[j] : 0;
         ((double*)out.car_x)[ix] = on ? K.cx[j] : 0.0;
         ((double*)out.car_y)[ix] = on ? K.cy[j] : 0.0;

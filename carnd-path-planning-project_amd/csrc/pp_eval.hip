@@ -110,14 +110,18 @@ __device__ __forceinline__ void st_xy(double* p, double x, double y) {
     __builtin_nontemporal_store(xy, (dv2*)p);
 }
 // ---- The output frame: the local -> global transform of TrajectoryBuilder::build (src/main.cpp:
-// 786-823, 994-1007, 1033-1037). It only maps points out (no decision of the loop reads it), so it
-// is evaluated in fused multiply-adds; every launch shape that writes points (k_cand emit_paths,
-// k_emit, the fused small-batch kernels, k_winner) calls these same functions, so their outputs
-// stay bit-identical to each other (and within ~1e-12 m of the reference's unfused sequence).
+// 786-823, 994-1007, 1033-1037). No decision of the loop reads it, so its turns (curvature
+// adjustments) are evaluated in fused multiply-adds with an angle-sum rotation of the heading; every
+// launch shape that writes points (k_cand emit_paths, k_emit, the fused small-batch kernels,
+// k_winner) calls these same functions, so their outputs stay bit-identical to each other (and
+// within ~1e-11 m of the reference after a turn, equal to it before the first one).
 struct OutFrame { double cx, cy, ca, sa; };   // centre, cos and sin of the frame's heading
+// a point: the reference's own operations (src/main.cpp:1033-1036), unfused: until a path's first
+// curvature adjustment its points carry the reference's bits, and in a closed loop those first
+// points are the next frame's previous path (its ego speed, heading and spline knots)
 __device__ __forceinline__ void frame_pt(const OutFrame& f, double px, double py, double& ox, double& oy) {
-    ox = __builtin_fma(px, f.ca, -(py * f.sa)) + f.cx;
-    oy = __builtin_fma(px, f.sa, py * f.ca) + f.cy;
+    ox = (px * f.ca - py * f.sa) + f.cx;
+    oy = (px * f.sa + py * f.ca) + f.cy;
 }
 // the turn of a curvature adjustment (src/main.cpp:986-997) at local point (px, py): the centre
 // rotates about the current output point, the heading's (cos, sin) by the angle-sum rotation
@@ -328,13 +332,17 @@ struct PlanAcc {
     int in_id; double in_s;
     int t_id[NL];
     double t_s[NL];
-    // iteration index of each running minimum, 6 bits each: next_s[l] at field l, the target-lane
+    // iteration index of each running minimum, kItBits each: next_s[l] at field l, the target-lane
     // car of lane l at field NL + l, the in-lane car at field 2 NL (the follow cars' velocities are
     // re-read from that index after the pass)
+    static constexpr int kItBits = 64 / (2 * NL + 1);
+    static constexpr uint64_t kItMask = (1ull << kItBits) - 1;
     uint64_t its;
     int nmatched;
-    __device__ __forceinline__ int it_of(int f) const { return (int)((its >> (6 * f)) & 63); }
-    __device__ __forceinline__ void set_it(int f, int it) { its = (its & ~(63ull << (6 * f))) | ((uint64_t)it << (6 * f)); }
+    __device__ __forceinline__ int it_of(int f) const { return (int)((its >> (kItBits * f)) & kItMask); }
+    __device__ __forceinline__ void set_it(int f, int it) {
+        its = (its & ~(kItMask << (kItBits * f))) | ((uint64_t)it << (kItBits * f));
+    }
     __device__ __forceinline__ void init() {
 #pragma unroll
         for (int l = 0; l < NL; l++) {
@@ -650,7 +658,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
             sorted = true;
         }
     }
-    static_assert((2 * NL + 1) * 6 <= 64 && PP_MAX_CARS <= 64, "iteration index fields");
+    static_assert(PP_MAX_CARS <= (1 << PlanAcc::kItBits), "iteration index fields");
     int p = 0;                              // next unread row (table mode)
     for (int kk = 0; kk < iters; kk++) {
         const int it = sorted ? (int)((order >> (4 * kk)) & 15) : kk;
@@ -2493,6 +2501,8 @@ void pp_params_default(pp_params* p) {
 int32_t pp_num_candidates(const pp_params* p) { return p ? n_draws(p) * NL * p->n_speeds : 0; }
 
 int32_t pp_num_lanes(void) { return NL; }
+
+int32_t pp_max_cars(void) { return PP_MAX_CARS; }
 
 double pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q) {
     return ppsynth::mc_gauss(seed, (uint64_t)scene, draw, car, q);

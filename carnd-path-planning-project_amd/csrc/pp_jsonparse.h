@@ -278,22 +278,26 @@ PP_HD int parse_frame(const R& r, int64_t len, K& sink) {
 }
 
 // Cars in std::map<int, Car> order (ascending id, the last row of an id wins), in place over
-// parallel arrays of n rows; returns the number of distinct ids. Stable insertion sort (n small).
-PP_HD inline int map_order(int* id, double* x, double* y, double* vx, double* vy, int n) {
+// parallel arrays of n rows (row i at element i * st); returns the number of distinct ids. Stable
+// insertion sort (n small).
+PP_HD inline int map_order(int* id, double* x, double* y, double* vx, double* vy, int n, int64_t st = 1) {
     for (int i = 1; i < n; i++) {
-        const int ki = id[i];
-        const double a = x[i], b = y[i], c = vx[i], d = vy[i];
+        const int ki = id[i * st];
+        const double a = x[i * st], b = y[i * st], c = vx[i * st], d = vy[i * st];
         int j = i - 1;
-        while (j >= 0 && id[j] > ki) {
-            id[j + 1] = id[j]; x[j + 1] = x[j]; y[j + 1] = y[j]; vx[j + 1] = vx[j]; vy[j + 1] = vy[j];
+        while (j >= 0 && id[j * st] > ki) {
+            const int64_t p = (j + 1) * st, q = j * st;
+            id[p] = id[q]; x[p] = x[q]; y[p] = y[q]; vx[p] = vx[q]; vy[p] = vy[q];
             j--;
         }
-        id[j + 1] = ki; x[j + 1] = a; y[j + 1] = b; vx[j + 1] = c; vy[j + 1] = d;
+        const int64_t p = (j + 1) * st;
+        id[p] = ki; x[p] = a; y[p] = b; vx[p] = c; vy[p] = d;
     }
     int u = 0;
     for (int i = 0; i < n; i++) {
-        if (i + 1 < n && id[i + 1] == id[i]) continue;        // a later row of the same id wins
-        id[u] = id[i]; x[u] = x[i]; y[u] = y[i]; vx[u] = vx[i]; vy[u] = vy[i];
+        if (i + 1 < n && id[(i + 1) * st] == id[i * st]) continue;        // a later row of the same id wins
+        const int64_t p = u * st, q = i * st;
+        id[p] = id[q]; x[p] = x[q]; y[p] = y[q]; vx[p] = vx[q]; vy[p] = vy[q];
         u++;
     }
     return u;

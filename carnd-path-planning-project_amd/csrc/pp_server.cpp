@@ -77,10 +77,13 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
     int64_t frames = 0, ticks = 0, accepted = 0, replies = 0;
     int32_t rc = PP_OK;
     const int cap = o->max_clients;
-    const int J = PP_MAX_CARS, N = prm.n_points, C = PP_NUM_LANES * prm.n_speeds;
-    // host batch (SoA, cap scenes) + results
-    std::vector<double> ego(4 * cap), pxy(2 * PP_PREV_KEEP * cap), cars(4 * J * cap), tabd(6 * PP_MAX_CARS * cap);
-    std::vector<int32_t> ints(3 * cap), cid(J * cap), tabi(3 * PP_MAX_CARS * cap), mst(cap);
+    const int N = prm.n_points, C = PP_NUM_LANES * prm.n_speeds;
+    // sensor_fusion columns of the host batch: grown (up to PP_MAX_CARS) when a frame reports more
+    // distinct cars than it holds, then the tick's frames are parsed again
+    int J = 16;
+    // host batch (SoA) + results, sized per tick
+    std::vector<double> ego, pxy, cars, tabd;
+    std::vector<int32_t> ints, cid, tabi, mst;
     std::vector<double> nxy(2 * N * cap), cost(C * cap);
     std::vector<int32_t> win(cap), nout(cap);
     std::vector<uint32_t> status(cap);
@@ -137,14 +140,24 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
             std::vector<int64_t> off(A + 1, 0);
             for (int i = 0; i < A; i++) { buf += batch[i]; off[i + 1] = (int64_t)buf.size(); }
             pp_scene_batch B;
-            memset(&B, 0, sizeof(B));
-            B.n_scenes = A; B.car_stride = J;
-            B.ego_x = ego.data(); B.ego_y = ego.data() + A; B.ego_yaw_deg = ego.data() + 2 * A; B.ego_speed_mph = ego.data() + 3 * A;
-            B.prev_x = pxy.data(); B.prev_y = pxy.data() + PP_PREV_KEEP * A;
-            B.n_prev = ints.data(); B.prev_target_lane = ints.data() + A; B.n_cars = ints.data() + 2 * A;
-            B.car_id = cid.data();
-            B.car_x = cars.data(); B.car_y = cars.data() + J * A; B.car_vx = cars.data() + 2 * J * A; B.car_vy = cars.data() + 3 * J * A;
-            rc = pp_telemetry_parse(buf.data(), off.data(), A, &B, mst.data(), o->threads);
+            mst.resize(A);
+            for (;;) {
+                ego.resize(4 * (size_t)A); pxy.resize(2 * PP_PREV_KEEP * (size_t)A); cars.resize(4 * (size_t)J * A);
+                ints.resize(3 * (size_t)A); cid.resize((size_t)J * A);
+                memset(&B, 0, sizeof(B));
+                B.n_scenes = A; B.car_stride = J;
+                B.ego_x = ego.data(); B.ego_y = ego.data() + A; B.ego_yaw_deg = ego.data() + 2 * A; B.ego_speed_mph = ego.data() + 3 * A;
+                B.prev_x = pxy.data(); B.prev_y = pxy.data() + PP_PREV_KEEP * A;
+                B.n_prev = ints.data(); B.prev_target_lane = ints.data() + A; B.n_cars = ints.data() + 2 * A;
+                B.car_id = cid.data();
+                B.car_x = cars.data(); B.car_y = cars.data() + J * A; B.car_vx = cars.data() + 2 * J * A; B.car_vy = cars.data() + 3 * J * A;
+                rc = pp_telemetry_parse(buf.data(), off.data(), A, &B, mst.data(), o->threads);
+                if (rc != PP_OK || J >= PP_MAX_CARS) break;
+                bool more = false;
+                for (int i = 0; i < A; i++) more |= mst[i] == 2;
+                if (!more) break;
+                J = std::min(2 * J, PP_MAX_CARS);
+            }
             if (rc != PP_OK) break;
             // dense batch of the telemetry frames, with each connection's state
             // status 2 (more distinct cars than PP_MAX_CARS) is not planned: the reference would
@@ -196,6 +209,8 @@ extern "C" int32_t pp_serve(pp_map* M, const pp_server_opts* o, volatile int32_t
                     TSl = std::max(TSl, used[i]);
                 }
                 D.tab_slots = TSl;
+                tabi.resize(3 * (size_t)TSl * T);
+                tabd.resize(6 * (size_t)TSl * T);
                 D.tab_id = tabi.data() + 2 * (size_t)TSl * T;
                 D.tab_valid = tabi.data(); D.tab_lane = tabi.data() + (size_t)TSl * T;
                 D.tab_s = tabd.data(); D.tab_d = tabd.data() + (size_t)TSl * T; D.tab_vs = tabd.data() + 2 * (size_t)TSl * T;

@@ -36,7 +36,8 @@ def _open():
 _LIB = _open()
 NUM_LANES = int(_LIB.pp_num_lanes())   # PP_NUM_LANES the library was built for (src/main.cpp:22)
 PREV_KEEP = 10
-MAX_CARS = 64            # PP_MAX_CARS: sensor_fusion rows and car-table slots per scene
+_LIB.pp_max_cars.restype = C.c_int32
+MAX_CARS = int(_LIB.pp_max_cars())     # PP_MAX_CARS: sensor_fusion rows and car-table slots per scene
 MAX_SPEEDS = 8
 MAX_POINTS = 128
 
@@ -134,7 +135,7 @@ EXPORTS = ["pp_params_default", "pp_num_candidates", "pp_version", "pp_map_creat
            "pp_mc_gauss", "pp_rollout", "pp_synth_traffic", "pp_synth_traffic_host", "pp_plan_reset",
            "pp_telemetry_parse", "pp_control_format", "pp_plan_batch_host", "pp_serve", "pp_ws_accept_key",
            "pp_telemetry_parse_device", "pp_control_format_device", "pp_map_create_device",
-           "pp_num_lanes", "pp_libm_eval", "pp_debug_set", "pp_debug_get"]
+           "pp_num_lanes", "pp_max_cars", "pp_libm_eval", "pp_debug_set", "pp_debug_get"]
 
 
 def _load():
@@ -394,8 +395,8 @@ def synth_traffic(m, S, seed=0x5EED0001, first=0, device=0, stream=None, car_str
     return d, t
 
 
-def synth_traffic_host(m, S, seed=0x5EED0001, first=0, car_stride=12):
-    d = add_car_table(alloc_scenes(S, car_stride))
+def synth_traffic_host(m, S, seed=0x5EED0001, first=0, car_stride=12, slots=12):
+    d = add_car_table(alloc_scenes(S, car_stride), slots=slots)
     t = alloc_traffic(S)
     b, T = scene_struct(d), traffic_struct(t)
     _check(lib.pp_synth_traffic_host(m.handle, seed, first, C.byref(b), C.byref(T)), "pp_synth_traffic_host")

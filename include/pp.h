@@ -34,7 +34,14 @@ extern "C" {
 #define PP_NUM_LANES   3    /* library is built for one value: pp_num_lanes() reports it)      */
 #endif
 #define PP_PREV_KEEP   10   /* src/main.cpp:1258 prev_trajectory_length                       */
-#define PP_MAX_CARS    64   /* sensor_fusion rows per scene and car-table slots (simulator: 12) */
+/* sensor_fusion rows per scene and car-table slots (the simulator reports 12; the reference's
+ * std::map<int, Car> has no bound, src/main.cpp:1194): 256 for up to three lanes, 64 beyond (the
+ * planner's order-dependent minima carry each winner's iteration index in a 64-bit word) */
+#if PP_NUM_LANES <= 3
+#define PP_MAX_CARS    256
+#else
+#define PP_MAX_CARS    64
+#endif
 #define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
 #define PP_MAX_POINTS  128  /* horizon N upper bound (reference: 50, src/main.cpp:854,1039)   */
 #define PP_MAX_KNOTS   16   /* spline knots: 9 prev + 1 + 5 control points (src/main.cpp:744) */
@@ -186,6 +193,7 @@ typedef struct pp_map pp_map;
 void    pp_params_default(pp_params* p);
 int32_t pp_num_candidates(const pp_params* p);
 int32_t pp_num_lanes(void);           /* PP_NUM_LANES of this build */
+int32_t pp_max_cars(void);            /* PP_MAX_CARS of this build */
 
 /* Map::Init (src/main.cpp:89-131) on the host (bit-identical to the reference's); the lane
  * geometry is uploaded lazily per device. n >= 3 waypoints, any size. */
@@ -324,8 +332,9 @@ int32_t pp_control_format(const double* next_x, const double* next_y, const int3
 /* The same codec on the GPU (one lane per frame; identical parser, number conversions and
  * writer). d_buf: the frames back to back in device memory, 16-byte aligned and readable up to
  * offsets[n] rounded up to 16; d_out: a DEVICE batch (n_scenes >= n_msgs). Statuses as above,
- * plus 4: the frame needs the host codec (a number outside the exact conversions' domain, more
- * than 24 sensor_fusion rows) — its fields are not written. Asynchronous on hip_stream. */
+ * plus 4: the frame needs the host codec (a number outside the exact conversions' domain, or more
+ * sensor_fusion rows than the batch's car_stride) — its fields are not written. Frames of any
+ * number of rows up to car_stride parse on the device. Asynchronous on hip_stream. */
 int32_t pp_telemetry_parse_device(const char* d_buf, const int64_t* d_offsets, int64_t n_msgs, pp_scene_batch* d_out,
                                   int32_t* d_status, int32_t device, void* hip_stream);
 /* Control messages on the GPU into fixed slots: message s = d_slots[s * slot_bytes, + d_len[s]);

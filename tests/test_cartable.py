@@ -196,6 +196,9 @@ class TestCarTableGPU:
         (list(range(1000, 1000 + 7 * 24, 7)), 60.0, 3, "stale"),   # 24 cars, ids >= 16, stale entries
         (sorted([-1, -9, 5, 17, 64, 99999, 2 ** 31 - 2, 12, 300, 301, 40, 41]), 1e5, 5, "erased"),
         (list(range(16, 40)), 45.0, 8, "stale"),
+        # 100 cars with sparse ids up to 2^31 - 2 (beyond the former 64-car limit)
+        (sorted(set([-(2 ** 31), -5, 0, 2 ** 31 - 2] + [int(v) for v in
+                    np.random.default_rng(77).choice(2 ** 31 - 3, 96, replace=False)])), 1e5, 9, "erased"),
     ])
     def test_plan_frame_episode_vs_reference(self, env, ids, sensor_range, seed, need):
         worst, stale, erased, rep = run_episode(env, ids, 300, seed, sensor_range)

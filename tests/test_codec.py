@@ -152,6 +152,36 @@ class TestDeviceCodec:
         n_ok, n_host = self.compare_parse(msgs)
         assert n_ok == 2000 and n_host == 0
 
+    def test_parse_many_rows_on_device(self):
+        """Frames with up to 250 sensor_fusion rows (duplicate and negative ids included) parse on
+        the GPU with a 256-column batch, bit for bit the host codec's std::map order; a frame with
+        more rows than the batch's columns goes to the host (status 4)."""
+        rng = np.random.default_rng(17)
+        msgs = []
+        for k, n in enumerate([0, 12, 24, 25, 40, 100, 180, 250, 256, 300]):
+            ids = rng.integers(-50, 400, n)
+            rows = ",".join("[%d,%r,%r,%r,%r,0,0]" % (int(i), float(rng.uniform(0, 3000)), float(rng.uniform(0, 3000)),
+                                                      float(rng.normal(0, 10)), float(rng.normal(0, 10)))
+                            for i in ids)
+            msgs.append(('42["telemetry",{"x":%r,"y":%r,"yaw":%r,"speed":%r,"previous_path_x":[1.5,2.5],'
+                         '"previous_path_y":[3.5,4.5],"sensor_fusion":[%s]}]'
+                         % (float(rng.uniform(0, 3000)), float(rng.uniform(0, 3000)), 12.5, 30.25, rows)).encode())
+        hd, hs = ppamd.telemetry_parse(msgs, car_stride=256)
+        dd, ds = ppamd.telemetry_parse_device(msgs, car_stride=256)
+        dd = {k: v.cpu().numpy() for k, v in dd.items()}
+        ds = ds.cpu().numpy()
+        # raw rows beyond the 256 columns: the device hands the frame to the host
+        assert ds[-1] == ppamd.MSG_HOST and ds[-2] in (0, ppamd.MSG_HOST)
+        on = ds != ppamd.MSG_HOST
+        assert on[:8].all() and (ds[on] == hs[on]).all()
+        assert hd["n_cars"][on].max() > 64
+        for k in hd:
+            a, b = np.asarray(hd[k])[..., on], dd[k][..., on]
+            if a.dtype.kind == "f":
+                assert (a.view(np.uint64) == b.view(np.uint64)).all(), k
+            else:
+                assert (a == b).all(), k
+
     def format_both(self, xs, ys, n_out):
         import torch
         want = ppamd.control_format(xs, ys, n_out)

@@ -70,6 +70,43 @@ def test_restatement_vs_reference_live(cpu, seed, consume, rng):
         np.testing.assert_array_equal(lo[k], lr[k], err_msg=k)
 
 
+def many_car_traffic(m, S, seed, n=100, dense=False):
+    """A rollout start with n cars (beyond the simulator's 12 and the former 64-car limit): the
+    synthetic start state's 12 cars plus n - 12 more around the whole loop (every 20th waypoint
+    segment, lanes rotated, other speeds), so a frame reports up to n rows of which the far ones
+    fail lane matching and leave the table. dense: the extra cars within +-12 segments of the start
+    instead (cars drive through each other and the ego: collisions, MAXBRAKE). Every car is in the
+    persistent table's id space (slots = n)."""
+    sc, tr = ppamd.synth_traffic_host(m, S, seed=seed, car_stride=n, slots=n)
+    nwp = m.geometry().shape[0]
+    big = ppamd.alloc_traffic(S, n=n)
+    for k in ("lane", "seg", "t", "offset", "speed"):
+        big[k][:12] = tr[k][:12]
+    for j in range(12, n):
+        b, r = j % 12, j // 12
+        big["lane"][j] = (tr["lane"][b] + r) % ppamd.NUM_LANES
+        big["seg"][j] = (tr["seg"][b] + (3 * r - 12 if dense else 20 * r)) % nwp
+        big["t"][j] = tr["t"][b]
+        big["offset"][j] = tr["offset"][b]
+        big["speed"][j] = tr["speed"][b] * (0.9 + 0.02 * r)
+    big["n_cars"] = n
+    return sc, big
+
+
+@pytest.mark.skipif(oracle_lib.load_ref() is None, reason="oracle/_ref not built (no reference here)")
+def test_restatement_vs_reference_100_cars(cpu):
+    """100 cars in the loop (more than the former 64-car limit): the restatement equals the
+    reference's own frame code (std::map car table) bit for bit over 300 frames."""
+    sc, tr = many_car_traffic(cpu["m"], 4, 21)
+    a, b = oracle_lib.copy_state(sc, tr), oracle_lib.copy_state(sc, tr)
+    lo = oracle_lib.oracle_rollout(cpu["olib"], cpu["wx"], cpu["wy"], *a, ppamd.default_params(n_speeds=1),
+                                   300, 3, 1e5)
+    lr = oracle_lib.ref_rollout(cpu["rlib"], cpu["wx"], cpu["wy"], *b, 300, 3, 1e5)
+    for k in LOG_KEYS + ["plan_x", "plan_y"]:
+        np.testing.assert_array_equal(lo[k], lr[k], err_msg=k)
+    assert lr["n_cars"].max() > 64, lr["n_cars"].max()
+
+
 @pytest.mark.gpu
 class TestRolloutGPU:
     @pytest.fixture(scope="class")
@@ -183,3 +220,62 @@ class TestRolloutGPU:
         assert ((tl >= 0) & (tl <= 2)).all()
         assert np.isfinite(lg["ego_x"].cpu().numpy()).all()
         assert (lg["n_out"].cpu().numpy()[1:] >= 40).mean() > 0.99
+
+    @pytest.mark.skipif(oracle_lib.load_ref() is None, reason="oracle/_ref not built")
+    def test_gpu_100_cars_vs_reference(self, env):
+        """100 cars (100 sensor_fusion rows every frame, a 100-slot car table) in the HIP closed
+        loop against the reference's own frame code over 300 frames: target lanes, point counts
+        and car counts exact, ego track and plans within 1e-6 m."""
+        sc, tr = many_car_traffic(env["m"], 64, 23)
+        a = oracle_lib.copy_state(sc, tr)
+        d, g = self.upload(env, sc, tr)
+        F, S = 300, 64
+        prm = ppamd.default_params(n_speeds=1)
+        res = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
+        lg = ppamd.alloc_log(F, S, 50, xp="torch", device=env["dev"])
+        ppamd.rollout(env["m"], d, g, prm, res, F, 3, 1e5, lg)
+        env["torch"].cuda.synchronize()
+        got = {k: x.cpu().numpy() for k, x in lg.items()}
+        lr = oracle_lib.ref_rollout(oracle_lib.load_ref(), env["wx"], env["wy"], *a, F, 3, 1e5)
+        for k in ["target_lane", "n_out", "n_cars"]:
+            np.testing.assert_array_equal(got[k], lr[k], err_msg=k)
+        e = 0.0
+        for k in ["ego_x", "ego_y", "plan_x", "plan_y"]:
+            e = max(e, float(np.abs(got[k] - lr[k]).max()))
+        assert e <= TOL, e
+        assert lr["n_cars"].max() > 64
+        print(f"100 cars: {S} scenes x {F} frames, up to {lr['n_cars'].max()} reported, max |d| {e:.2e} m")
+
+    def test_gpu_100_dense_cars_frame_by_frame(self, env):
+        """Dense 100-car traffic (cars drive through each other and the ego): every frame of a GPU
+        episode re-run by the restatement from the GPU's own state (the reference-pinned
+        restatement, tests/test_rollout.py::test_restatement_vs_reference_100_cars): target lanes
+        and point counts exact, plans within 1e-6 m, the car table identical. (A free-running
+        comparison of such traffic is chaotic: an ulp in a fed-back point meets near-ties of the
+        collision and braking rules.)"""
+        t = env["torch"]
+        S, F = 64, 150
+        sc, tr = many_car_traffic(env["m"], S, 23, dense=True)
+        d, g = self.upload(env, sc, tr)
+        prm = ppamd.default_params(n_speeds=1)
+        res = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
+        worst, rows = 0.0, 0
+        for f in range(F):
+            hs = {k: x.cpu().numpy() for k, x in d.items()}
+            ht = {k: (x.cpu().numpy() if isinstance(x, t.Tensor) else x) for k, x in g.items()}
+            lo = oracle_lib.oracle_rollout(env["olib"], env["wx"], env["wy"], hs, ht, prm, 1, 3, 400.0)
+            lg = ppamd.alloc_log(1, S, 50, xp="torch", device=env["dev"])
+            ppamd.rollout(env["m"], d, g, prm, res, 1, 3, 400.0, lg)
+            t.cuda.synchronize()
+            got = {k: x.cpu().numpy() for k, x in lg.items()}
+            np.testing.assert_array_equal(got["target_lane"], lo["target_lane"], err_msg=str(f))
+            np.testing.assert_array_equal(got["n_out"], lo["n_out"], err_msg=str(f))
+            for k in ["plan_x", "plan_y"]:
+                worst = max(worst, float(np.abs(got[k] - lo[k]).max()))
+            new = {k: x.cpu().numpy() for k, x in d.items()}
+            for k in ("tab_valid", "tab_lane", "n_cars", "car_id"):
+                np.testing.assert_array_equal(new[k], hs[k], err_msg=f"{f} {k}")
+            rows = max(rows, int(new["n_cars"].max()))
+        assert worst <= TOL, worst
+        assert rows > 64, rows
+        print(f"dense 100 cars: {S} scenes x {F} frames, up to {rows} rows, max |dxy| {worst:.2e} m")
