@@ -238,95 +238,8 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
 
 // lane_matching on a map with fastm: the same walk, with each lane segment's rdenom and its
 // reciprocal from the tables (the division snom^2 / rdenom by div_by_rcp: the same correctly
-// rounded value), and the waypoint indices stepped instead of re-wrapped.
-__device__ inline bool lane_matching_tab(const MapV& m, int ref_wp, const double ratio[NL], double x,
-                                         double y, double& out_s, double& out_d, int& out_lane,
-                                         int& out_next_wp) {
-    const int n = m.n;
-    int dir = 0;
-    bool stop = false;
-    int cur = ref_wp;
-    int a = wpi(cur - 1, n), b = wpi(cur, n);
-    double sum_s[NL], sr[NL];
-#pragma unroll
-    for (int l = 0; l < NL; l++) { sum_s[l] = 0; sr[l] = ratio[l]; }
-    double best = 1000 * 1000;
-    bool found = false;
-    int b_lane = 0, b_cur = 0, b_b = 0;
-    double b_rnom = 0, b_snom = 0, b_ss = 0, b_sr = 0;
-    for (int it = 0; it < 4 * n + 8; it++) {
-        PP_DIAGC(16, true);
-        bool improved = false;
-#pragma unroll
-        for (int lane = 0; lane < NL; lane++) {
-            const double ax = m.lc_x[lane * n + a], ay = m.lc_y[lane * n + a];
-            const double bx = m.lc_x[lane * n + b], by = m.lc_y[lane * n + b];
-            const double den = m.lden[lane * n + b];
-            const double pdx = x - ax, dx = bx - ax;                    // helpers.h:203-207
-            const double pdy = y - ay, dy = by - ay;
-            const double rn = pdx * dx + pdy * dy;
-            const double snom = pdx * dy - pdy * dx;
-            double rnom, dsq;
-            if (rn < -1) { rnom = 0; dsq = pdx * pdx + pdy * pdy; }                            // :227-231
-            else if (rn > den) { rnom = den; dsq = (x - bx) * (x - bx) + (y - by) * (y - by); }   // :232-236
-            else { rnom = rn; dsq = div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]); }
-            if (dsq < best) {
-                best = dsq;
-                improved = true;
-                found = true;
-                b_lane = lane;
-                b_cur = cur;
-                b_b = b;
-                b_rnom = rnom; b_snom = snom;
-                b_sr = sr[lane];
-                b_ss = sum_s[lane];
-            }
-            if (rnom == 0) {
-                if (dir == 1) stop = true;
-                dir = -1;
-            } else if (rnom == den) {
-                if (dir == -1) stop = true;
-                dir = 1;
-            } else {
-                stop = true;
-            }
-        }
-        if (!improved || stop) break;
-        double ll[NL];
-#pragma unroll
-        for (int l = 0; l < NL; l++) ll[l] = m.llen[l * n + b];
-        if (dir > 0) {
-#pragma unroll
-            for (int l = 0; l < NL; l++) { sum_s[l] += (1 - sr[l]) * ll[l]; sr[l] = 0; }
-            cur++;
-            a = b;
-            b = b + 1 == n ? 0 : b + 1;
-        } else {
-#pragma unroll
-            for (int l = 0; l < NL; l++) { sum_s[l] -= sr[l] * ll[l]; sr[l] = 1; }
-            cur--;
-            b = a;
-            a = a == 0 ? n - 1 : a - 1;
-        }
-        // below -n the reference's size_t wrap (src/main.cpp:134-137) is not a plain modulus
-        if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
-    }
-    if (found) {                                                   // :214-227, last improvement
-        const double b_rdenom = m.lden[b_lane * n + b_b];
-        const double rfs = b_rnom / b_rdenom;
-        const double r_mod = rfs - b_sr;
-        const double seg_len = m.llen[b_lane * n + b_b];
-        out_s = b_ss + seg_len * r_mod;
-        double d = sqrt(best);
-        if (b_snom < 0) d = -d;
-        out_d = d + lane_offset(b_lane);
-        out_lane = b_lane;
-        out_next_wp = b_cur;
-    }
-    return found;
-}
-
-// lane_matching_tab with lighter bookkeeping (same walk, same arithmetic, same results):
+// rounded value), the waypoint indices stepped instead of re-wrapped, and lighter bookkeeping
+// (same arithmetic, same results):
 // - the walk is monotone (a direction change stops it, :237-246), so a segment's end points are
 //   carried to the next iteration (forward: b becomes a; backward: a becomes b) and only the new
 //   point is loaded;
@@ -425,77 +338,10 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
     return found;
 }
 
-// ---- lane_matching in two passes (k_prep's flattened car loop) ----
-// Pass 1 only walks: per car it keeps the walk's outcome (found, lane and segment of the last
-// improvement) in a 16-bit word. Pass 2 rebuilds s and d of that projection by the walk's own
-// operations: the distance and the projection terms of the recorded (lane, segment), and the
-// lane's running sum_s over the segments from ref_wp to that segment (the walk is monotone, so the
-// ratio shift is ratio[lane] at ref_wp, 0 after forward steps, 1 after backward ones: :255-272).
-// Same values as lane_matching_tab2, bit for bit.
-// word: bit 15 found, bits 12-14 lane, bits 0-11 (segment - ref_wp) + 2048; kWalkRedo: the
-// segment lies beyond that range (pass 2 runs lane_matching_tab2 itself); 0: no projection.
-constexpr uint16_t kWalkRedo = 0x7000;
-
-// one lane segment's squared distance and clamped projection (helpers.h:188-249 with the tables;
-// the same operations as lane_matching_tab2's walk)
-__device__ __forceinline__ double seg_dsq(const MapV& m, int lane, int a, int b, double x, double y,
-                                          double& rnom, double& snom, double& den) {
-    const int n = m.n;
-    const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
-    const double pbx = m.lc_x[lane * n + b], pby = m.lc_y[lane * n + b];
-    den = m.lden[lane * n + b];
-    const double pdx = x - pax, dx = pbx - pax;
-    const double pdy = y - pay, dy = pby - pay;
-    const double rn = pdx * dx + pdy * dy;
-    snom = pdx * dy - pdy * dx;
-    if (rn < -1) { rnom = 0; return pdx * pdx + pdy * pdy; }
-    if (rn > den) { rnom = den; return (x - pbx) * (x - pbx) + (y - pby) * (y - pby); }
-    rnom = rn;
-    return div_by_rcp(snom * snom, den, m.lrcp[lane * n + b]);
-}
-
-// pass 2: s, d, lane and next waypoint of the projection a pass-1 word records (found bit set)
-__device__ __forceinline__ void walk_finish(const MapV& m, int ref_wp, const double ratio[NL], double x,
-                                            double y, uint32_t w, double& out_s, double& out_d,
-                                            int& out_lane, int& out_next_wp) {
-    const int n = m.n;
-    const int l = (int)((w >> 12) & 7);
-    const int kc = ref_wp + (int)(w & 0xFFF) - 2048;
-    // the lane's running sum_s and ratio shift when the walk stood at segment kc (:255-272)
-    double sr = ratio[0];
-    asm("" : "+v"(sr));                       // a select chain, not an indexed (scratch) load
-#pragma unroll
-    for (int i = 1; i < NL; i++) {
-        double ri = ratio[i];
-        asm("" : "+v"(ri));
-        sr = l == i ? ri : sr;
-    }
-    double ss = 0;
-    if (kc > ref_wp) {
-        for (int c = ref_wp; c < kc; c++) { ss += (1 - sr) * m.llen[l * n + wpi(c, n)]; sr = 0; }
-    } else if (kc < ref_wp) {
-        for (int c = ref_wp; c > kc; c--) { ss -= sr * m.llen[l * n + wpi(c, n)]; sr = 1; }
-    }
-    const int b = wpi(kc, n), a = wpi(kc - 1, n);
-    double rnom, snom, den;
-    const double dsq = seg_dsq(m, l, a, b, x, y, rnom, snom, den);
-    const double r_mod = rnom / den - sr;
-    out_s = ss + m.llen[l * n + b] * r_mod;
-    double d = sqrt(dsq);
-    if (snom < 0) d = -d;
-    out_d = d + lane_offset(l);
-    out_lane = l;
-    out_next_wp = kc;
-}
-
 __device__ __forceinline__ bool lane_match(const MapV& m, int ref_wp, const double ratio[NL], double x,
                                            double y, double& out_s, double& out_d, int& out_lane,
                                            int& out_next_wp) {
-#ifndef PP_MATCH_TAB
-#define PP_MATCH_TAB 2
-#endif
-    if (PP_MATCH_TAB == 2 && m.fastm) return lane_matching_tab2(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
-    if (PP_MATCH_TAB && m.fastm) return lane_matching_tab(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
+    if (m.fastm) return lane_matching_tab2(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
     return lane_matching(m, ref_wp, ratio, x, y, out_s, out_d, out_lane, out_next_wp);
 }
 

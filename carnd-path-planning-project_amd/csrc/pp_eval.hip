@@ -112,9 +112,10 @@ __device__ __forceinline__ void st_xy(double* p, double x, double y) {
 // ---- The output frame: the local -> global transform of TrajectoryBuilder::build (src/main.cpp:
 // 786-823, 994-1007, 1033-1037). No decision of the loop reads it, so its turns (curvature
 // adjustments) are evaluated in fused multiply-adds with an angle-sum rotation of the heading; every
-// launch shape that writes points (k_cand emit_paths, k_emit, the fused small-batch kernels,
-// k_winner) calls these same functions, so their outputs stay bit-identical to each other (and
-// within ~1e-11 m of the reference after a turn, equal to it before the first one).
+// launch shape that writes the reference decision's next_x/next_y (k_emit, the fused small-batch
+// kernels) or a winner's (k_winner) calls these same functions, so their outputs stay bit-identical
+// to each other (and within ~1e-11 m of the reference after a turn, equal to it before the first
+// one). k_cand's all-paths mode has a cheaper variant below (frame_pt_fma, frame_turn_at).
 struct OutFrame { double cx, cy, ca, sa; };   // centre, cos and sin of the frame's heading
 // a point: the reference's own operations (src/main.cpp:1033-1036), unfused: until a path's first
 // curvature adjustment its points carry the reference's bits, and in a closed loop those first
@@ -188,6 +189,33 @@ __device__ __forceinline__ void turn_sincos(double r, double& s, double& c) {
     }
 }
 
+// k_cand's all-paths mode (output mode 4): the same output frame, cheaper. Every candidate writes
+// its path there, so the point transform runs on every lane-step and a turn on about half of all
+// wave-steps (for one lane in ten): each point is two fused multiply-adds per coordinate
+// (frame_pt_fma); the loop keeps the last output point o, so a turn sets the centre from it — c = o -
+// R' p, the current point keeps its output — instead of rotating the old centre about o; the turn
+// angle's reciprocal takes one Newton step. ~1e-13 m from the shared turn (frame_turn); the paths' tolerance is 1e-6 m, and
+// no decision and no closed loop reads these points (the reference decision's next_x/next_y and
+// every fed-back path come from frame_turn / k_emit).
+__device__ __forceinline__ void frame_turn_at(OutFrame& f, double px, double py, double ox, double oy,
+                                              double cr, double sr) {
+    const double nca = __builtin_fma(f.ca, cr, -(f.sa * sr)), nsa = __builtin_fma(f.sa, cr, f.ca * sr);
+    f.ca = nca;
+    f.sa = nsa;
+    f.cx = ox - __builtin_fma(nca, px, -(nsa * py));
+    f.cy = oy - __builtin_fma(nsa, px, nca * py);
+}
+__device__ __forceinline__ void frame_pt_fma(const OutFrame& f, double px, double py, double& ox, double& oy) {
+    ox = __builtin_fma(px, f.ca, __builtin_fma(-py, f.sa, f.cx));
+    oy = __builtin_fma(px, f.sa, __builtin_fma(py, f.ca, f.cy));
+}
+__device__ __forceinline__ double turn_angle_fast(double nc, double speed, double adiff) {
+    double r = __builtin_amdgcn_rcp(speed);
+    r = __builtin_fma(__builtin_fma(-speed, r, 1.0), r, r);
+    double nad = (nc * 0.02) * r;          // (speed, hence nad, may be negative)
+    if (adiff < 0) nad = -nad;
+    return nad - adiff;
+}
 // Tuning constants (each measured against its alternatives):
 constexpr int kEmitChunk = 4;      // k_emit: recorded steps loaded together per lane (large batches)
 constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
@@ -1169,7 +1197,8 @@ struct CandRes { double acc_sum, travelled; int ng; uint32_t flags; uint64_t adj
 // Output modes. The curvature adjustment (src/main.cpp:972-1018) rotates only the local->global
 // transform (centre, angle); the local path (pos_x, pos_y, arg, speed, angles) that the cost reads
 // never depends on it, so a cost-only lane skips the transform, its sin/cos and the stores.
-//   kOutMode 0: cost only;  2: every lane produces points;  3: lanes with out_on RECORD their local path (pos after each step, rotation angle of each
+//   kOutMode 0: cost only;  2: every lane produces points;  4: the same with k_cand's cheaper
+//   output-frame turn (frame_turn_at);  3: lanes with out_on RECORD their local path (pos after each step, rotation angle of each
 //   curvature adjustment + a bitmask of the adjusted steps) for k_emit, which replays the
 //   transform — the expensive sin/cos of the adjustments leaves the candidate loop entirely.
 // Point g goes to wx[g*ws], wy[g*ws] (if wx) and px[g*ps], px[g*ps+1] (if px); in mode 3 the record
@@ -1183,7 +1212,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                                  double* rec = nullptr, int dcls = 0, int64_t rs = 0) {
     (void)dcls;   // PP_DIAG builds: candidate class (|L - ego lane|) for the census
     // kOutMode 3: rec = the record base + rs (the scene), ws = the batch's scene count (rec_st)
-    const bool kOut = kOutMode == 2;
+    const bool kOut = kOutMode == 2 || kOutMode == 4;
     const bool kRec = kOutMode == 3 && out_on;
     const int64_t rstride = (int64_t)room * ws;
     CandRes R;
@@ -1193,6 +1222,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     if (mflags & kMetaWalkFail) R.flags |= PP_ST_NAN;
     double pos_x = 0, pos_y = 0;
     OutFrame F = {cx, cy, ca0, sa0};
+    double opx = cx, opy = cy;        // mode 4: the last output point (the frame's image of (0, 0))
     (void)angle;      // the frame turns by rotating (ca, sa) (src/main.cpp:996-997)
     double cur_t = 0.02;
     int ng = 0;
@@ -1329,8 +1359,10 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
         if (acc + cacc > P.maximum_acc) {
             if (speed > prev_speed) {                                   // :945-971
+                // (inside this block acc + cacc > max held: neither is NaN; k_cand<false>'s
+                // operands are finite, so the clamp is v_max_f64)
                 double na = P.maximum_acc - cacc;
-                if (na < 0) na = 0;
+                if (kLarge) { if (na < 0) na = 0; } else na = __builtin_fmax(na, 0.0);
                 const double ns = prev_speed + PP_DIV50(na);
                 sc_override_r<kLarge>(sc, cur_t, ns, rds);
                 speed = ns;
@@ -1343,12 +1375,16 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             PP_DIAGC(6, acc + cacc > P.maximum_acc);
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
                 double nc = P.maximum_acc - acc;
-                if (nc < 0) nc = 0;
-                if (kOutMode != 0 && kOut) {
+                if (kLarge) { if (nc < 0) nc = 0; } else nc = __builtin_fmax(nc, 0.0);
+                if (kOutMode == 2) {
                     // the output frame turns about the current point (src/main.cpp:986-997)
                     double cr, sr;
                     turn_sincos<kLarge>(turn_angle<kLarge>(nc, speed, adiff), sr, cr);
                     frame_turn(F, pos_x, pos_y, cr, sr);
+                } else if (kOutMode == 4) {
+                    double cr, sr;
+                    turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), sr, cr);
+                    frame_turn_at(F, pos_x, pos_y, opx, opy, cr, sr);
                 }
                 if (kOutMode == 3 && kRec) {
                     // the turn angle for k_emit's replay of the output frame
@@ -1381,10 +1417,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
         if (kOutMode != 0 && kOut) {
             double ox, oy;
-            frame_pt(F, pos_x, pos_y, ox, oy);
+            if (kOutMode == 4) frame_pt_fma(F, pos_x, pos_y, ox, oy);
+            else frame_pt(F, pos_x, pos_y, ox, oy);
             if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = ox; wy[ng * ws] = oy; }
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
+            if (kOutMode == 4) { opx = ox; opy = oy; }
         }
         if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
         ng++;
@@ -1632,7 +1670,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 st_xy(p0 + i * ps, in.prev_x[(int64_t)i * S + s], in.prev_y[(int64_t)i * S + s]);
             }
             double* px = p0 + K * ps;
-            R = run_candidate<kSlow, 2>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
+            R = run_candidate<kSlow, 4>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
                                                        pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
                                                        px, ps);
             for (int i = R.ng; i < N - K; i++) {
