@@ -236,6 +236,55 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
     return an == 0.0 ? q0 : q;
 }
 
+// One walk iteration's segment (a, b) is an *approach* segment when every lane's projection is
+// clamped to the end the walk moves towards (rn > rdenom forward, rn < -1 backward: the walk goes
+// on in the same direction, src/main.cpp:237-246), with rdenom >= 1 m^2 and the point within 1e5 m
+// of a: then every lane's squared distance at this iteration is below its value at the previous one
+// by more than rdenom minus the rounding of rn (exact: |p-a|^2 - |p-b|^2 = 2 (rn - rdenom) + rdenom),
+// far more than the rounding of the distances themselves (< 1e-5 m^2 there), so the iteration
+// improves the running minimum whatever it was. rn is computed by the walk's own operations.
+#ifndef PP_WALK_APPROACH
+#define PP_WALK_APPROACH 1
+#endif
+__device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double x, double y, int dir) {
+    const int n = m.n;
+    bool ok = true;
+#pragma unroll
+    for (int lane = 0; lane < NL; lane++) {
+        const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
+        const double pbx = m.lc_x[lane * n + b], pby = m.lc_y[lane * n + b];
+        const double den = m.lden[lane * n + b];
+        const double pdx = x - pax, dx = pbx - pax;
+        const double pdy = y - pay, dy = pby - pay;
+        const double rn = pdx * dx + pdy * dy;
+        ok = ok && (dir > 0 ? rn > den : rn < -1) && den >= 1.0 && fabs(pdx) < 1e5 && fabs(pdy) < 1e5;
+    }
+    return ok;
+}
+// commits approach segments from iteration `it` (segment (a, b), an approach segment) while the
+// next one is one too; returns the iteration the full walk resumes at (its segment uncommitted)
+__device__ __forceinline__ int approach_walk(const MapV& m, double x, double y, int dir, int& a, int& b,
+                                             int& cur, double sum_s[NL], double sr[NL], int it) {
+    const int n = m.n;
+    for (;;) {
+        if (it + 2 >= 4 * n + 8 || cur - 2 < -n) break;
+        int a2, b2;
+        if (dir > 0) { a2 = b; b2 = b + 1 == n ? 0 : b + 1; }
+        else { b2 = a; a2 = a == 0 ? n - 1 : a - 1; }
+        if (!approach_seg(m, a2, b2, x, y, dir)) break;
+        PP_DIAGC(16, true);
+#pragma unroll
+        for (int l = 0; l < NL; l++) {
+            if (dir > 0) { sum_s[l] += (1 - sr[l]) * m.llen[l * n + b]; sr[l] = 0; }
+            else { sum_s[l] -= sr[l] * m.llen[l * n + b]; sr[l] = 1; }
+        }
+        cur += dir;
+        a = a2; b = b2;
+        it++;
+    }
+    return it;
+}
+
 // lane_matching on a map with fastm: the same walk, with each lane segment's rdenom and its
 // reciprocal from the tables (the division snom^2 / rdenom by div_by_rcp: the same correctly
 // rounded value), the waypoint indices stepped instead of re-wrapped, and lighter bookkeeping
@@ -245,7 +294,14 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
 //   point is loaded;
 // - an improvement records only its lane (and the best distance); the iteration's segment, the
 //   lane's running sum_s and ratio shift are kept once per improving iteration, and the recorded
-//   projection's rnom/snom are recomputed after the walk by the same operations.
+//   projection's rnom/snom are recomputed after the walk by the same operations;
+// - a run of approach segments (approach_seg) is walked by its clamp tests and the sum_s
+//   bookkeeping alone: each improves and goes on (nothing recorded there is read, since the next
+//   iteration improves too), so only the last one before a segment that is not an approach segment
+//   runs in full — it improves against any running minimum at least the true one (the kept
+//   first-iteration minimum), and records the lane of its own minimum, as the full walk does.
+//   The run starts after the first iteration (which sets the direction and a minimum below the
+//   initial 1000^2) and stops one segment early.
 __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const double ratio[NL], double x,
                                           double y, double& out_s, double& out_d, int& out_lane,
                                           int& out_next_wp) {
@@ -314,6 +370,8 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             a = a == 0 ? n - 1 : a - 1;
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
         }
+        if (PP_WALK_APPROACH && it == 0 && approach_seg(m, a, b, x, y, dir))
+            it = approach_walk(m, x, y, dir, a, b, cur, sum_s, sr, it + 1) - 1;
     }
     if (found) {                                                   // :214-227, last improvement
         const int l = b_lane;
