@@ -238,8 +238,9 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
 
 // One walk iteration's segment (a, b) is an *approach* segment when every lane's projection is
 // clamped to the end the walk moves towards (rn > rdenom forward, rn < -1 backward: the walk goes
-// on in the same direction, src/main.cpp:237-246), with rdenom >= 1 m^2 and the point within 1e5 m
-// of a: then every lane's squared distance at this iteration is below its value at the previous one
+// on in the same direction, src/main.cpp:237-246), on a map whose lane segments all have rdenom >=
+// 1 m^2 and lane centres within 4e4 m of the origin (MapV::fastm bit 2, checked once per map) for a
+// point within 5e4 m of it (so within 1e5 m of every lane point; checked once per walk): then every lane's squared distance at this iteration is below its value at the previous one
 // by more than rdenom minus the rounding of rn (exact: |p-a|^2 - |p-b|^2 = 2 (rn - rdenom) + rdenom),
 // far more than the rounding of the distances themselves (< 1e-5 m^2 there), so the iteration
 // improves the running minimum whatever it was. rn is computed by the walk's own operations.
@@ -257,7 +258,7 @@ __device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double
         const double pdx = x - pax, dx = pbx - pax;
         const double pdy = y - pay, dy = pby - pay;
         const double rn = pdx * dx + pdy * dy;
-        ok = ok && (dir > 0 ? rn > den : rn < -1) && den >= 1.0 && fabs(pdx) < 1e5 && fabs(pdy) < 1e5;
+        ok = ok && (dir > 0 ? rn > den : rn < -1);
     }
     return ok;
 }
@@ -370,7 +371,8 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             a = a == 0 ? n - 1 : a - 1;
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
         }
-        if (PP_WALK_APPROACH && it == 0 && approach_seg(m, a, b, x, y, dir))
+        if (PP_WALK_APPROACH && it == 0 && (m.fastm & 2) && fabs(x) < 5e4 && fabs(y) < 5e4 &&
+            approach_seg(m, a, b, x, y, dir))
             it = approach_walk(m, x, y, dir, a, b, cur, sum_s, sr, it + 1) - 1;
     }
     if (found) {                                                   // :214-227, last improvement

@@ -217,7 +217,8 @@ __device__ __forceinline__ double turn_angle_fast(double nc, double speed, doubl
     return nad - adiff;
 }
 // Tuning constants (each measured against its alternatives):
-constexpr int kEmitChunk = 4;      // k_emit: recorded steps loaded together per lane (large batches)
+constexpr int kEmitChunk = 4;      // emit_scene_pre (small batches): recorded steps loaded together per lane
+constexpr int kEmitRows = 8;       // k_emit (large batches, emit_scene_rows): output rows per load round
 constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
 constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
 constexpr int kCandWaves = 4;      // k_cand waves per SIMD (<= 128 VGPRs)
@@ -1931,12 +1932,108 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
     for (int i = K + ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
 }
 
+// k_emit by output rows: the lane's loop runs over next_x/next_y's rows i = 0 .. N-1 (kept previous
+// point i < K, generated point g = i - K < ng, zero after), so every store of the wave goes to one
+// row (512 contiguous bytes), where stepping by g scatters each store over the rows K + g of the
+// wave's lanes (K = 0 ... 9) and leaves every written line partial. The record loads are the ones
+// scattered instead (rows g = i - K), read through the cache, where the wave's other lanes of the
+// same line find them. Same operations in the same order per lane as emit_scene: bit-identical.
+template <int kChunk>
+__device__ __forceinline__ void emit_scene_rows(const pp_scene_batch& in, const pp_params& P, const PrepV& pv,
+                                                const pp_result& out, const double* rec, const uint64_t* adjm,
+                                                int64_t s) {
+    const int64_t S = in.n_scenes;
+    const int N = P.n_points;
+    const int K = pv.K[s];
+    const int room = N - K;
+    const int ng = out.n_out[s] - K;
+    const int64_t rstride = (int64_t)room * S;
+    OutFrame F = {pv.pos_x[s], pv.pos_y[s], pv.ca_p[s], pv.sa_p[s]};
+    const uint64_t m0 = adjm[s], m1 = adjm[S + s];
+    double pxp = 0, pyp = 0;                       // local position before the step
+    for (int i0 = 0; i0 < N; i0 += kChunk) {
+        double px_[kChunk], py_[kChunk], rt[kChunk];
+        uint32_t bits = 0, gen = 0;
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            const int i = i0 + u, g = i - K;
+            const bool isg = i < N && g >= 0 && g < ng;
+            const bool bit = isg && ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0);
+            bits |= bit ? 1u << u : 0u;
+            gen |= isg ? 1u << u : 0u;
+#ifdef PP_CHECK
+            if (isg) { PP_CHKP(rec_py((double*)rec, rstride, g, S, s), rec, nrec, 16); }
+            if (bit) { PP_CHKP(rec_rot(rec, rstride, g, S, s), rec, nrec, 16); }
+#endif
+            px_[u] = 0.0; py_[u] = 0.0;
+            if (isg) {
+                px_[u] = *rec_px((double*)rec, rstride, g, S, s);
+                py_[u] = *rec_py((double*)rec, rstride, g, S, s);
+            } else if (i < K) {
+                px_[u] = in.prev_x[(int64_t)i * S + s];
+                py_[u] = in.prev_y[(int64_t)i * S + s];
+            }
+            rt[u] = bit ? *rec_rot(rec, rstride, g, S, s) : 0.0;
+        }
+        bool huge = false;
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) huge |= !(fabs(rt[u]) <= ppm::kMediumMax);
+        if (__builtin_expect(huge, 0)) {
+            // a turn beyond the medium range: the chunk step by step with the library reduction,
+            // re-reading its inputs (the unrolled path below then holds no call)
+            for (int i = i0; i < N && i < i0 + kChunk; i++) {
+                const int g = i - K;
+                double ox = 0.0, oy = 0.0;
+                if (g >= 0 && g < ng) {
+                    if ((g < 64 ? (m0 >> g) & 1 : (m1 >> (g - 64)) & 1) != 0) {
+                        double cr, sr;
+                        turn_sincos<true>(*rec_rot(rec, rstride, g, S, s), sr, cr);
+                        frame_turn(F, pxp, pyp, cr, sr);
+                    }
+                    const double qx = *rec_px((double*)rec, rstride, g, S, s);
+                    const double qy = *rec_py((double*)rec, rstride, g, S, s);
+                    frame_pt(F, qx, qy, ox, oy);
+                    pxp = qx;
+                    pyp = qy;
+                } else if (i < K) {
+                    ox = in.prev_x[(int64_t)i * S + s];
+                    oy = in.prev_y[(int64_t)i * S + s];
+                }
+                out.next_x[(int64_t)i * S + s] = ox;
+                out.next_y[(int64_t)i * S + s] = oy;
+            }
+            continue;
+        }
+        double crs[kChunk], srs[kChunk];
+        if (bits) {
+#pragma unroll
+            for (int u = 0; u < kChunk; u++) turn_sincos<false>(rt[u], srs[u], crs[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            const int i = i0 + u;
+            if (i >= N) break;
+            double ox = px_[u], oy = py_[u];
+            if ((gen >> u) & 1) {
+                if ((bits >> u) & 1) frame_turn(F, pxp, pyp, crs[u], srs[u]);
+                frame_pt(F, px_[u], py_[u], ox, oy);
+                pxp = px_[u];
+                pyp = py_[u];
+            }
+            if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 17)) break;
+            PP_ST(out.next_x + (int64_t)i * S + s, ox);
+            PP_ST(out.next_y + (int64_t)i * S + s, oy);
+        }
+    }
+}
+
 template <int kChunk>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                               const double* rec, const uint64_t* adjm, int64_t s0, int64_t s1) {
     const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // scenes [s0, s1)
     if (s >= s1 || s >= in.n_scenes) return;
-    emit_scene<kChunk>(in, P, pv, out, rec, adjm, s);
+    if (kChunk == kEmitRows) emit_scene_rows<kChunk>(in, P, pv, out, rec, adjm, s);
+    else emit_scene<kChunk>(in, P, pv, out, rec, adjm, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2215,7 +2312,7 @@ struct pp_map {
     std::vector<double> geom;     // kMapArrays * n (MapG layout)
     std::vector<double> ptab;     // (4 + 2 NL) * n: ref xy, normal, lane centres (pp_map_geometry)
     std::vector<double> lanetab;  // 5 NL * n
-    int fastm = 0;                // MapV::fastm: every lane segment's rdenom in [2^-500, 2^500]
+    int fastm = 0;                // MapV::fastm: bit 1: every lane segment's rdenom in [2^-500, 2^500]; bit 2: approach_seg's map bounds
     DevState dev[kMaxDev];
     std::mutex mu;
 };
@@ -2241,6 +2338,12 @@ void fill_ptab(pp_map* M) {
     M->fastm = 1;
     for (size_t i = (size_t)(4 + 3 * NL) * n; i < (size_t)(4 + 4 * NL) * n; i++)
         if (!(g[i] >= 0x1p-500 && g[i] <= 0x1p500)) M->fastm = 0;
+    // bit 2 (lane matching's approach runs, pp_device.h approach_seg): every lane segment's rdenom
+    // >= 1 m^2 and every lane centre within 4e4 m of the origin
+    bool appr = M->fastm != 0;
+    for (size_t i = (size_t)(4 + 3 * NL) * n; i < (size_t)(4 + 4 * NL) * n; i++) appr = appr && g[i] >= 1.0;
+    for (size_t i = (size_t)4 * n; i < (size_t)(4 + 2 * NL) * n; i++) appr = appr && std::fabs(g[i]) < 4e4;
+    if (appr) M->fastm |= 2;
 }
 
 // Map::Init (src/main.cpp:89-131) + derived tables, on the host (done once per map).
@@ -2882,7 +2985,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             hipLaunchKernelGGL(k_emit<16>, dim3((unsigned)blocks), dim3(64), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         } else {
             const int64_t blocks = (S + 255) / 256;
-            hipLaunchKernelGGL(k_emit<kEmitChunk>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
+            hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)blocks), dim3(256), 0, st, B, P, pv, R, rec, adjm, (int64_t)0, S);
         }
     }
     // K3 (comfort mode, or any mode with draws): argmin + winner path
