@@ -22,17 +22,75 @@ import mpmath as mp
 LIBM = sys.argv[1] if len(sys.argv) > 1 else "/lib/x86_64-linux-gnu/libm.so.6"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "carnd-path-planning-project_amd", "csrc", "pp_glibc_tables.h")
-# table offsets in glibc 2.35-0ubuntu3.11's libm.so.6 (.rodata, file offset == vaddr), found
-# from the x86-64 FMA variants' table loads (__sin_fma: lea 0xaeb80; __atan2_fma: lea 0xbe0e0)
-SINCOS_OFF, SINCOS_N = 0xAEB80, 440
-ATAN_OFF, ATAN_N = 0xBE0E0, 241 * 7
+SINCOS_N = 440
+ATAN_N = 241 * 7
+# where glibc 2.35-0ubuntu3.11's libm.so.6 holds them (.rodata, file offset == vaddr; the x86-64
+# FMA variants' table loads: __sin_fma lea 0xaeb80, __atan2_fma lea 0xbe0e0). Any other build is
+# searched by content (find_tables), and every entry is checked against mpmath either way.
+KNOWN_OFFSETS = (0xAEB80, 0xBE0E0)
 
 mp.mp.prec = 200
+
+
+def sincos_ok(data, off):
+    if off < 0 or off + 8 * SINCOS_N > len(data):
+        return False
+    sc = struct.unpack_from("<%dd" % SINCOS_N, data, off)
+    for i in range(SINCOS_N // 4):
+        x = mp.mpf(i) / 128
+        for k, f in ((0, mp.sin), (2, mp.cos)):
+            v = f(x)
+            if sc[4 * i + k] != float(v) or abs(mp.mpf(sc[4 * i + k]) + mp.mpf(sc[4 * i + k + 1]) - v) >= mp.mpf(2) ** -100:
+                return False
+    return True
+
+
+def atan_ok(data, off):
+    if off < 0 or off + 8 * ATAN_N > len(data):
+        return False
+    at = struct.unpack_from("<%dd" % ATAN_N, data, off)
+    for j in range(ATAN_N // 7):
+        e = at[7 * j:7 * j + 7]
+        c = mp.mpf(e[0])
+        if not (abs(c - mp.mpf(j + 16) / 256) < mp.mpf(2) ** -8 and abs(mp.mpf(e[1]) - mp.atan(c)) < mp.mpf(2) ** -60
+                and abs(mp.mpf(e[2]) - 1 / (1 + c * c)) < mp.mpf(2) ** -50):
+            return False
+    return True
+
+
+def find_tables(data):
+    """File offsets of __sincostab and the atan table: the known ones when they hold the tables,
+    else a content search (the sine table's second row, sin(1/128)'s double, 32 bytes in; the atan
+    table's first centre, a double within 2^-8 of 1/16 followed by its atan), each candidate
+    accepted only if every entry passes the mpmath checks. (2.35 keeps one copy of the atan table
+    per ifunc variant of atan2; the copies are byte-identical, so any of them will do.)"""
+    so, ao = KNOWN_OFFSETS
+    if not sincos_ok(data, so):
+        key = struct.pack("<d", float(mp.sin(mp.mpf(1) / 128)))
+        so, i = None, data.find(key)
+        while i >= 0 and so is None:
+            if (i - 32) % 8 == 0 and sincos_ok(data, i - 32):
+                so = i - 32
+            i = data.find(key, i + 1)
+        if so is None:
+            raise SystemExit("gen_glibc_tables: __sincostab not found in " + LIBM)
+    if not atan_ok(data, ao):
+        ao = None
+        for i in range(0, len(data) - 16, 8):
+            c = struct.unpack_from("<d", data, i)[0]
+            if 0.0586 < c < 0.0665 and abs(struct.unpack_from("<d", data, i + 8)[0] - float(mp.atan(c))) < 1e-15:
+                if atan_ok(data, i):
+                    ao = i
+                    break
+        if ao is None:
+            raise SystemExit("gen_glibc_tables: the atan table was not found in " + LIBM)
+    return so, ao
 
 
 def main():
     data = open(LIBM, "rb").read()
     sha = hashlib.sha256(data).hexdigest()
+    SINCOS_OFF, ATAN_OFF = find_tables(data)
     sc = struct.unpack("<%dd" % SINCOS_N, data[SINCOS_OFF:SINCOS_OFF + 8 * SINCOS_N])
     at = struct.unpack("<%dd" % ATAN_N, data[ATAN_OFF:ATAN_OFF + 8 * ATAN_N])
     # sincostab: hi parts are the correctly rounded sin/cos of i/128, lo parts within 2^-100 of
@@ -52,7 +110,7 @@ def main():
         assert abs(mp.mpf(e[2]) - 1 / (1 + c * c)) < mp.mpf(2) ** -50, j
     lines = [
         "// pp_glibc_tables.h — GENERATED by tools/gen_glibc_tables.py; do not edit.",
-        "// Data tables of the libm the reference links (glibc 2.35 x86-64, %s, sha256 %s):" % (os.path.basename(LIBM), sha),
+        "// Data tables of the libm the reference links (glibc 2.35 x86-64, %s, sha256 %s, offsets 0x%x 0x%x):" % (os.path.basename(LIBM), sha, SINCOS_OFF, ATAN_OFF),
         "// s_sin.c's __sincostab (sin/cos of i/128 as hi + lo) and e_atan2.c's accurate atan table",
         "// (centre, atan(centre), Taylor coefficients). Used by pp_glibcm.h.",
         "#pragma once",
