@@ -269,7 +269,7 @@ def test_full_size_properties(env):
 def test_prep_group_invariance(env, case):
     """K1 runs one lane per evaluation on large batches (cars nearest first) and a group of G lanes
     per evaluation on small ones (rows split over the group, planner in row order): every G
-    (pp_set_prep_group) gives bit-identical outputs, and G = 1 and G = 16 equal the oracle. Cases:
+    (pp_debug_set(PP_DBG_PREP_GROUP, G)) gives bit-identical outputs, and G = 1 and G = 16 equal the oracle. Cases:
     random scenes; tied duplicate cars with -1, negative and large ids; 24 rows (more than one
     round per group); Monte-Carlo draws (one group per scene x draw)."""
     import test_cartable
