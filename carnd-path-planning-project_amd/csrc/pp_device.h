@@ -247,9 +247,9 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
 #ifndef PP_WALK_APPROACH
 #define PP_WALK_APPROACH 1
 #endif
-__device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double x, double y, int dir) {
+__device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double x, double y, bool fwd) {
     const int n = m.n;
-    bool ok = true;
+    bool okf = true, okb = true;          // every lane's test, no short circuit (no branches)
 #pragma unroll
     for (int lane = 0; lane < NL; lane++) {
         const double pax = m.lc_x[lane * n + a], pay = m.lc_y[lane * n + a];
@@ -258,26 +258,29 @@ __device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double
         const double pdx = x - pax, dx = pbx - pax;
         const double pdy = y - pay, dy = pby - pay;
         const double rn = pdx * dx + pdy * dy;
-        ok = ok && (dir > 0 ? rn > den : rn < -1);
+        okf &= rn > den;
+        okb &= rn < -1;
     }
-    return ok;
+    return fwd ? okf : okb;
 }
 // commits approach segments from iteration `it` (segment (a, b), an approach segment) while the
-// next one is one too; returns the iteration the full walk resumes at (its segment uncommitted)
+// next one is one too; returns the iteration the full walk resumes at (its segment uncommitted).
+// After the walk's first step the ratio shift sr is 0 forward and 1 backward, so a commit adds or
+// subtracts the segment length exactly ((1 - 0) l = l, 1 l = l; x - l == x + (-l)).
 __device__ __forceinline__ int approach_walk(const MapV& m, double x, double y, int dir, int& a, int& b,
-                                             int& cur, double sum_s[NL], double sr[NL], int it) {
+                                             int& cur, double sum_s[NL], int it) {
     const int n = m.n;
+    const bool fwd = dir > 0;
     for (;;) {
         if (it + 2 >= 4 * n + 8 || cur - 2 < -n) break;
-        int a2, b2;
-        if (dir > 0) { a2 = b; b2 = b + 1 == n ? 0 : b + 1; }
-        else { b2 = a; a2 = a == 0 ? n - 1 : a - 1; }
-        if (!approach_seg(m, a2, b2, x, y, dir)) break;
+        const int a2 = fwd ? b : (a == 0 ? n - 1 : a - 1);
+        const int b2 = fwd ? (b + 1 == n ? 0 : b + 1) : a;
+        if (!approach_seg(m, a2, b2, x, y, fwd)) break;
         PP_DIAGC(16, true);
 #pragma unroll
         for (int l = 0; l < NL; l++) {
-            if (dir > 0) { sum_s[l] += (1 - sr[l]) * m.llen[l * n + b]; sr[l] = 0; }
-            else { sum_s[l] -= sr[l] * m.llen[l * n + b]; sr[l] = 1; }
+            const double len = m.llen[l * n + b];
+            sum_s[l] += fwd ? len : -len;
         }
         cur += dir;
         a = a2; b = b2;
@@ -372,8 +375,8 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
         }
         if (PP_WALK_APPROACH && it == 0 && (m.fastm & 2) && fabs(x) < 5e4 && fabs(y) < 5e4 &&
-            approach_seg(m, a, b, x, y, dir))
-            it = approach_walk(m, x, y, dir, a, b, cur, sum_s, sr, it + 1) - 1;
+            approach_seg(m, a, b, x, y, dir > 0))
+            it = approach_walk(m, x, y, dir, a, b, cur, sum_s, it + 1) - 1;
     }
     if (found) {                                                   // :214-227, last improvement
         const int l = b_lane;
