@@ -19,10 +19,7 @@ namespace ppd {
 
 constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
 constexpr double kEps = 1e-5;                     // src/main.cpp:24
-#ifndef PP_KKP
-#define PP_KKP 17
-#endif
-constexpr int kKP = PP_KKP;                       // LDS knot stride (16 knots + 1 pad: bank spread)
+constexpr int kKP = 17;                       // LDS knot stride (16 knots + 1 pad: bank spread)
 static_assert(kKP >= 15, "a slot holds npk + ncp <= (PP_PREV_KEEP - 1) + 6 = 15 knots");
 constexpr int NL = PP_NUM_LANES;                  // lanes (src/main.cpp:22)
 // ref x/y, normal x/y, lane centre x[NL]/y[NL], length[NL], segment |.|^2 [NL] and its reciprocal [NL]
@@ -244,9 +241,6 @@ __device__ __forceinline__ double div_by_rcp(double n, double d, double r) {
 // by more than rdenom minus the rounding of rn (exact: |p-a|^2 - |p-b|^2 = 2 (rn - rdenom) + rdenom),
 // far more than the rounding of the distances themselves (< 1e-5 m^2 there), so the iteration
 // improves the running minimum whatever it was. rn is computed by the walk's own operations.
-#ifndef PP_WALK_APPROACH
-#define PP_WALK_APPROACH 1
-#endif
 __device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double x, double y, bool fwd) {
     const int n = m.n;
     bool okf = true, okb = true;          // every lane's test, no short circuit (no branches)
@@ -374,7 +368,7 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             a = a == 0 ? n - 1 : a - 1;
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
         }
-        if (PP_WALK_APPROACH && it == 0 && (m.fastm & 2) && fabs(x) < 5e4 && fabs(y) < 5e4 &&
+        if (it == 0 && (m.fastm & 2) && fabs(x) < 5e4 && fabs(y) < 5e4 &&
             approach_seg(m, a, b, x, y, dir > 0))
             it = approach_walk(m, x, y, dir, a, b, cur, sum_s, it + 1) - 1;
     }

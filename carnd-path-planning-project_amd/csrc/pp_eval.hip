@@ -2551,7 +2551,7 @@ int ensure_ws(StreamWS& W, hipStream_t st, int64_t Sv) {
 }
 
 int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
-    const int64_t cap = (S + 63) & ~(int64_t)63;   // whole 64-scene blocks (PP_REC_PAIR 2)
+    const int64_t cap = (S + 63) & ~(int64_t)63;   // whole 64-scene blocks
     if (W.rec_cap >= cap) return PP_OK;
     if (W.rec) { (void)hipStreamSynchronize(st); (void)hipFree(W.rec); W.rec = nullptr; W.rec_cap = 0; }
     if (hipMalloc(&W.rec, rec_bytes(cap)) != hipSuccess) return PP_ERR_NOMEM;
