@@ -2027,8 +2027,11 @@ __device__ __forceinline__ void emit_scene_rows(const pp_scene_batch& in, const 
     }
 }
 
+// 4 waves per SIMD (128 VGPRs): the 262,144-scene shard's k_emit 0.108 -> 0.098 ms, the full
+// config-5 batch unchanged (profiles/r03_ablations.txt)
+constexpr int kEmitWaves = 4;
 template <int kChunk>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kEmitWaves))) void k_emit(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                               const double* rec, const uint64_t* adjm, int64_t s0, int64_t s1) {
     const int64_t s = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // scenes [s0, s1)
     if (s >= s1 || s >= in.n_scenes) return;
