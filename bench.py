@@ -145,6 +145,18 @@ def workload_name(S, Cn, n_speeds, N, emit_paths, D, rollout):
     return "custom workload"
 
 
+def workload_scope(wname, S, total, world, scaling):
+    """How the run's scenes relate to the named workload: the whole config-5 batch sharded over the
+    ranks, one rank-sized shard of it measured alone (e.g. 262,144 scenes = its share at N = 8), or
+    a fixed batch per GPU."""
+    if scaling == "weak":
+        return f" ({S} per GPU)"
+    if wname == "BASELINE config 5" and total != CONFIG5_SCENES:
+        return (f" (one shard of the {CONFIG5_SCENES}-scene batch: its share at N = {CONFIG5_SCENES // total}"
+                if CONFIG5_SCENES % total == 0 else " (a partial batch") + f", measured on {world} GPU(s))"
+    return f" sharded over {world} GPUs"
+
+
 def roofline_fields(pmc, cands_launch, bpc, k_ms):
     """traffic (dominant kernel) and traffic_pipeline (every kernel of a step) per launch of this
     run, from the PMC entry's bytes per candidate."""
@@ -184,7 +196,7 @@ def parse(argv=None):
                     help="chunks of the host-buffer pipeline (H2D / evaluate / D2H overlapped across chunks)")
     ap.add_argument("--debug", action="append", default=[], metavar="KEY=VALUE",
                     help="library debug switch for A/B runs (include/pp.h PP_DBG_*): prep_group=G, "
-                         "prep_waves=3|4, shape=1|2|3; never part of a reported bench line")
+                         "prep_waves=3|4, shape=1|2|3; recorded in config.debug, which marks the line not reportable")
     ap.add_argument("--cpu-ranks", action="store_true",
                     help="launcher rehearsal without a GPU: every rank evaluates its shard with the CPU oracle")
     return ap.parse_args(argv)
@@ -584,7 +596,7 @@ def main(argv=None):
         "config": {"workload": (f"{wname}: {total_scenes} scenes x {D} sensor-noise draws x 3 lanes x "
                                 f"{a.n_speeds} speeds, per-scene argmin over draws" if D > 1 else
                                 f"{wname}: {total_scenes} scenes x 3 lanes x {a.n_speeds} speeds")
-                               + (f" sharded over {world} GPUs" if a.scaling == "strong" else f" ({S} per GPU)")
+                               + workload_scope(wname, S, total_scenes, world, a.scaling)
                                + f", {a.n_points}-pt horizon"
                                + (", all paths emitted" if a.emit_paths else ", winner path + costs")
                                + (f", closed loop: {a.rollout} frames per step (plan + simulator, 3 points "
@@ -592,7 +604,9 @@ def main(argv=None):
                                + (", comfort cost" if a.comfort else ", reference decision"),
                    "scenes_total": total_scenes, "scenes_per_gpu": S, "candidates_per_scene": Cn,
                    "horizon_points": a.n_points,
-                   "parallelism": f"contiguous scene shards x{world}, no collective (gloo barrier + max for timing)"},
+                   "parallelism": f"contiguous scene shards x{world}, no collective (gloo barrier + max for timing)",
+                   **({"debug": dict(kv.partition("=")[::2] for kv in a.debug), "reportable": False}
+                      if a.debug else {})},
         "kernels_ms_avg": {k: kms[k] for k in ("k_prep", "k_cand", "k_out")},
         "per_rank_kernels_ms": per_rank,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -61,11 +61,12 @@ PP_HD inline void philox4x32(uint64_t seed, uint64_t scene, uint32_t block, uint
 }
 
 // Monte-Carlo sensor noise (include/pp.h pp_mc_gauss): Irwin-Hall of four 32-bit uniforms of one
-// Philox block, counter {scene, (draw * PP_MAX_CARS + car) * 4 + q, 0x4D43}; unit variance; exactly rounded
+// Philox block, counter {scene, (draw * PP_NOISE_CAR_STRIDE + car) * 4 + q, 0x4D43}; unit variance; exactly rounded
 // arithmetic only, so host and device agree bit for bit.
+static_assert(PP_MAX_CARS <= PP_NOISE_CAR_STRIDE, "noise counter stride below the car limit");
 PP_HD inline double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, int q) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)(((draw * PP_MAX_CARS) + car) * 4 + q), 0x4D43u};
+    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)(((draw * PP_NOISE_CAR_STRIDE) + car) * 4 + q), 0x4D43u};
     for (int r = 0; r < 10; r++) {
         philox_round(ctr, key);
         key[0] += 0x9E3779B9u;

@@ -42,6 +42,9 @@ extern "C" {
 #else
 #define PP_MAX_CARS    64
 #endif
+/* the Monte-Carlo noise counter's car stride (pp_mc_gauss): fixed, so a seed draws the same noise
+ * in every build whatever its PP_MAX_CARS (which never exceeds it) */
+#define PP_NOISE_CAR_STRIDE 256
 #define PP_MAX_SPEEDS  8    /* target speeds per lane                                          */
 #define PP_MAX_POINTS  128  /* horizon N upper bound (reference: 50, src/main.cpp:854,1039)   */
 #define PP_MAX_KNOTS   16   /* spline knots: 9 prev + 1 + 5 control points (src/main.cpp:744) */
@@ -401,7 +404,7 @@ int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches
 
 /* The Monte-Carlo noise generator (host copy of the device code; bit-identical): standard-normal-
  * like variate q (0..3 -> x, y, vx, vy) of car j in draw d of global scene `scene`. Irwin-Hall of
- * four 32-bit Philox4x32-10 uniforms (key = seed, counter = {scene, (d*PP_MAX_CARS + j)*4 + q,
+ * four 32-bit Philox4x32-10 uniforms (key = seed, counter = {scene, (d*PP_NOISE_CAR_STRIDE + j)*4 + q,
  * 0x4D43}), scaled to unit variance: only exactly rounded arithmetic, no libm. */
 double  pp_mc_gauss(uint64_t seed, int64_t scene, int32_t draw, int32_t car, int32_t q);
 

@@ -516,11 +516,11 @@ typedef struct {
 static const uint32_t limit_flag[5] = {0, PP_ST_BRAKE, PP_ST_MAXBRAKE, PP_ST_ADJUST, PP_ST_KEEP};
 
 /* Monte-Carlo sensor noise (build extension, include/pp.h pp_params / pp_mc_gauss): Philox4x32-10
- * block keyed by the seed, counter {scene, (draw * PP_MAX_CARS + car) * 4 + q, 0x4D43}; Irwin-Hall of its
+ * block keyed by the seed, counter {scene, (draw * PP_NOISE_CAR_STRIDE + car) * 4 + q, 0x4D43}; Irwin-Hall of its
  * four 32-bit uniforms scaled to unit variance. */
 static double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, int q) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)((draw * PP_MAX_CARS + car) * 4 + q), 0x4D43u};
+    uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)((draw * PP_NOISE_CAR_STRIDE + car) * 4 + q), 0x4D43u};
     for (int r = 0; r < 10; r++) {
         uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0], p1 = (uint64_t)0xCD9E8D57u * ctr[2];
         uint32_t n0 = (uint32_t)(p1 >> 32) ^ ctr[1] ^ key[0];

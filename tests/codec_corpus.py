@@ -90,3 +90,56 @@ def control_values(seed, n):
                         np.round(rng.uniform(-1000, 1000, n)), [0.0, -0.0, np.nan, np.inf, -np.inf, 1e15, 1e16,
                                                                  123456789012345.0, 5e-324, 1.7976931348623157e308, 0.1]])
     return v
+
+
+def sim_spell(rng, v):
+    """The spellings a simulator-side JSON writer produces (at most 17 significant digits)."""
+    k = rng.integers(0, 5)
+    if k == 0:
+        return "%.15g" % v
+    if k == 1:
+        return "%.17g" % v
+    if k == 2:
+        return "%.6f" % v
+    if k == 3 and abs(v) < 1e6:
+        return str(int(v))
+    return repr(float(v))
+
+
+def sim_corpus(seed, n):
+    """Simulator-shaped telemetry: every number within the device codec's exact domain (so the GPU
+    parses every frame itself), 12 cars, 0-47 previous points, a manual frame every 16th."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for m in range(n):
+        if m % 16 == 15:
+            out.append(b'42["telemetry",null]' if m % 32 == 15 else b'42["manual",{}]')
+            continue
+        sp = lambda v: sim_spell(rng, v)
+        n_prev = int(rng.choice([0, 10, 47]))
+        x, y = rng.uniform(0, 3000), rng.uniform(0, 3000)
+        px = x + np.cumsum(rng.uniform(0, 0.45, n_prev))
+        py = y + np.cumsum(rng.uniform(-0.05, 0.05, n_prev))
+        rows = ",".join("[%d,%s,%s,%s,%s,%s,%s]" % (j, sp(rng.uniform(0, 3000)), sp(rng.uniform(0, 3000)),
+                                                    sp(rng.uniform(-25, 25)), sp(rng.uniform(-25, 25)),
+                                                    sp(rng.uniform(0, 7000)), sp(rng.uniform(0, 12)))
+                        for j in range(12))
+        out.append(('42["telemetry",{"x":%s,"y":%s,"yaw":%s,"speed":%s,"s":%s,"d":%s,"previous_path_x":[%s],'
+                    '"previous_path_y":[%s],"end_path_s":%s,"end_path_d":%s,"sensor_fusion":[%s]}]'
+                    % (sp(x), sp(y), sp(rng.uniform(0, 360)), sp(rng.uniform(0, 50)), sp(rng.uniform(0, 7000)),
+                       sp(rng.uniform(0, 12)), ",".join(sp(v) for v in px), ",".join(sp(v) for v in py),
+                       sp(rng.uniform(0, 7000)), sp(rng.uniform(0, 12)), rows)).encode())
+    return out
+
+
+def trajectory_values(seed, N, S):
+    """Planner-like next_x/next_y (point-major [N][S]): magnitudes 1e-3..1e6, some integral values,
+    some NaN (the control dump's `null`)."""
+    rng = np.random.default_rng(seed)
+    xs = rng.uniform(-3000, 3000, (N, S)) * 10.0 ** rng.integers(-3, 4, (N, S))
+    xs[::7] = np.round(xs[::7])
+    xs[::11, ::3] = np.nan
+    ys = rng.uniform(-3000, 3000, (N, S))
+    n_out = rng.integers(0, N + 1, S).astype(np.int32)
+    n_out[:4] = (0, 1, N, N)
+    return xs, ys, n_out

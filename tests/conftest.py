@@ -15,8 +15,12 @@ def pytest_configure(config):
     # every pp_eval of the test run starts from NaN-filled intermediates and outputs and checks
     # that the slow-group bitmap is clear (include/pp.h PP_DBG_POISON), so no kernel can pass a
     # test on what an earlier call left there; PP_TEST_NO_POISON=1 runs the suite without it
+    # (oracle-only CPU sessions do not need the library: poison matters only where it loads)
     if os.environ.get("PP_TEST_NO_POISON") != "1":
-        import ppamd
+        try:
+            import ppamd
+        except (ImportError, OSError):
+            return
         ppamd.debug_set(ppamd.DBG_POISON, 1)
 
 

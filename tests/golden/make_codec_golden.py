@@ -30,12 +30,33 @@ def main():
     off = np.cumsum([0] + [len(m) for m in msgs])
     dbuf = b"".join(dumps)
     doff = np.cumsum([0] + [len(d) for d in dumps])
+    # simulator-shaped frames the GPU codec parses itself, and planner-like control dumps it formats
+    # itself: the reference's fields / bytes for the device codec's direct parity test
+    smsgs = codec_corpus.sim_corpus(2025, 512)
+    sst, sego, spx, spy, snpv, sids, scars = [], [], [], [], [], [], []
+    for m in smsgs:
+        s, e, a, b, n, i, c = oracle_lib.ref_json_parse(rj, m)
+        assert s != 0 or len(i) == 12
+        sst.append(s); sego.append(e); spx.append(a); spy.append(b); snpv.append(n)
+        ii = np.zeros(12, np.int32); cc = np.zeros((12, 4)); ii[:len(i)] = i; cc[:len(i)] = c
+        sids.append(ii); scars.append(cc)
+    txs, tys, tn = codec_corpus.trajectory_values(2026, 50, 96)
+    tdumps = [oracle_lib.ref_json_dump(rj, txs[:tn[k], k], tys[:tn[k], k]) for k in range(len(tn))]
+    sbuf = b"".join(smsgs)
+    soff = np.cumsum([0] + [len(m) for m in smsgs])
+    tbuf = b"".join(tdumps)
+    toff = np.cumsum([0] + [len(d) for d in tdumps])
     np.savez_compressed(os.path.join(HERE, "codec_golden.npz"),
+                        sim_buf=np.frombuffer(sbuf, np.uint8), sim_off=soff, sim_status=np.array(sst, np.int32),
+                        sim_ego=np.array(sego), sim_prev_x=np.array(spx), sim_prev_y=np.array(spy),
+                        sim_n_prev=np.array(snpv, np.int32), sim_car_id=np.array(sids), sim_cars=np.array(scars),
+                        traj_x=txs, traj_y=tys, traj_n=tn, traj_buf=np.frombuffer(tbuf, np.uint8), traj_off=toff,
                         msg_buf=np.frombuffer(buf, np.uint8), msg_off=off, status=np.array(st, np.int32),
                         ego=np.array(ego), prev_x=np.array(px), prev_y=np.array(py), n_prev=np.array(npv, np.int32),
                         n_cars=np.array(ncar, np.int32), car_id=np.array(ids), cars=np.array(cars),
                         values=vals, dump_buf=np.frombuffer(dbuf, np.uint8), dump_off=doff)
-    print(f"{len(msgs)} frames ({int(np.sum(np.array(st) == 0))} telemetry), {len(dumps)} control messages")
+    print(f"{len(msgs)} frames ({int(np.sum(np.array(st) == 0))} telemetry), {len(dumps)} control messages; "
+          f"{len(smsgs)} simulator-shaped frames, {len(tdumps)} trajectory dumps")
 
 
 if __name__ == "__main__":

@@ -14,7 +14,9 @@
   (16,384 noisy evaluations) against the restatement;
 - config 5: 2,097,152 scenes (test_gpu_parity.py::test_full_size_properties, and the bench).
 The restatement (oracle/pp_oracle.c) is pinned bit for bit to the reference's own code
-(tests/test_oracle.py); N = 100 has no reference counterpart (it hard-codes 50 points)."""
+(tests/test_oracle.py); at N = 100 too, through oracle/_ref/libppref_n.so (the reference with its
+two point-count literals, src/main.cpp:854 and :1039, made settable) and the committed fixture
+tests/golden/golden_config3.npz (tests/test_golden_n.py, which also tiles it into a large GPU batch)."""
 import numpy as np
 import pytest
 

@@ -67,6 +67,33 @@ def test_format_matches_reference_fixture():
         assert got[i] == buf[off[i]:off[i + 1]], i
 
 
+def sim_msgs():
+    buf = G["sim_buf"].tobytes()
+    off = G["sim_off"]
+    return [buf[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+def sim_ref(s):
+    return (int(G["sim_status"][s]), G["sim_ego"][s], G["sim_prev_x"][s], G["sim_prev_y"][s],
+            int(G["sim_n_prev"][s]), G["sim_car_id"][s], G["sim_cars"][s])
+
+
+def traj_dumps():
+    buf, off = G["traj_buf"].tobytes(), G["traj_off"]
+    return [buf[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+
+
+def test_sim_fixture_host_codec():
+    """Simulator-shaped frames and planner-like dumps (the reference's fields and bytes in the
+    fixture's sim_* / traj_* arrays): the host codec, bit and byte for byte."""
+    msgs = sim_msgs()
+    d, st = ppamd.telemetry_parse(msgs, car_stride=12)
+    for s in range(len(msgs)):
+        check_frame(d, st, s, sim_ref(s))
+    got = ppamd.control_format(G["traj_x"], G["traj_y"], G["traj_n"])
+    assert got == traj_dumps()
+
+
 def test_format_roundtrip_through_parse():
     """Control output parsed back as the next frame's previous path recovers at least %.15g."""
     rng = np.random.default_rng(3)
@@ -115,8 +142,42 @@ def test_parse_and_format_vs_reference_live(seed):
 
 @pytest.mark.gpu
 class TestDeviceCodec:
-    """The GPU codec (pp_codec.hip) against the host codec: same statuses (the device hands frames
-    with libc-only numbers to the host: status 4), same bits, same bytes."""
+    """The GPU codec (pp_codec.hip) against the reference's own outputs (codec_golden.npz, made by
+    the reference's hasData + json.hpp) and against the host codec: same statuses (the device hands
+    frames with libc-only numbers to the host: status 4), same bits, same bytes."""
+
+    def test_parse_vs_reference_fixture(self):
+        """Device-parsed fields == the reference's (src/helpers.h:15-25, src/main.cpp:1225-1252
+        via json.hpp), bit for bit: the simulator-shaped frames all on the GPU, and the adversarial
+        corpus's frames wherever the device does not hand them to the host."""
+        msgs = sim_msgs()
+        dd, ds = ppamd.telemetry_parse_device(msgs, car_stride=12)
+        dd = {k: v.cpu().numpy() for k, v in dd.items()}
+        ds = ds.cpu().numpy()
+        assert (ds != ppamd.MSG_HOST).all()
+        for s in range(len(msgs)):
+            check_frame(dd, ds, s, sim_ref(s))
+        msgs = golden_msgs()
+        dd, ds = ppamd.telemetry_parse_device(msgs, car_stride=16)
+        dd = {k: v.cpu().numpy() for k, v in dd.items()}
+        ds = ds.cpu().numpy()
+        on = np.flatnonzero(ds != ppamd.MSG_HOST)
+        assert len(on) > 0
+        for s in on:
+            n = int(G["n_cars"][s])
+            check_frame(dd, ds, s, (int(G["status"][s]), G["ego"][s], G["prev_x"][s], G["prev_y"][s],
+                                    int(G["n_prev"][s]), G["car_id"][s][:n], G["cars"][s][:n]))
+
+    def test_format_vs_reference_fixture(self):
+        """Device-formatted control messages == the reference's msgJson.dump() bytes
+        (src/main.cpp:1461-1466, json.hpp:6689-6692 %.15g): planner-like values all on the GPU."""
+        import torch
+        dev = torch.device("cuda", 0)
+        slots, ln = ppamd.control_format_device(torch.from_numpy(G["traj_x"]).to(dev),
+                                                torch.from_numpy(G["traj_y"]).to(dev),
+                                                torch.from_numpy(G["traj_n"]).to(dev))
+        got = ppamd.slots_to_messages(slots, ln)
+        assert got == traj_dumps()
 
     def compare_parse(self, msgs):
         hd, hs = ppamd.telemetry_parse(msgs, car_stride=16)
