@@ -71,6 +71,24 @@ constexpr int kMetaPoison = 0x7fffffff;
 #define PP_CHKP(p, B, N, site) true
 #define PP_CHK(ok, site, off) true
 #endif
+#ifdef PP_TRACE
+// diagnostic builds only (-DPP_TRACE): per workgroup of the traced kernel (k_cand<false>, and k_prep
+// at kTraceK1 + blockIdx), 8 words: [0] start, [1] end of phase A, [2..5] end of phase B per wave,
+// [6] end, [7] XCC id << 32 | HW_ID; times from the 100 MHz constant clock. Read with pp_trace_read.
+constexpr int kTraceMax = 1 << 18, kTraceK1 = 3 << 16;
+__device__ unsigned long long g_trace[8 * kTraceMax];
+__device__ __forceinline__ void trace_at(unsigned long long blk, int k) {   // blk < kTraceMax
+    g_trace[8 * blk + k] = wall_clock64();
+}
+__device__ __forceinline__ unsigned long long trace_hwid() {
+    const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));    // HW_REG_XCC_ID
+    return ((unsigned long long)xcc << 32) | hw;
+}
+#define PP_TRACE_AT(blk, k) do { if ((blk) < (unsigned)kTraceK1) trace_at((blk), (k)); } while (0)
+#else
+#define PP_TRACE_AT(blk, k) ((void)0)
+#endif
 #include "pp_device.h"
 #include "pp_glibcm.h"
 #include "pp_math.h"
@@ -615,10 +633,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
                                               int64_t v0, int64_t v1) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
+#ifdef PP_TRACE
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1)) {
+        trace_at(kTraceK1 + blockIdx.x, 0);
+        g_trace[8 * (kTraceK1 + blockIdx.x) + 7] = trace_hwid();
+    }
+#endif
     if (kLdsMap) {
         for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
         __syncthreads();
     }
+#ifdef PP_TRACE
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1)) trace_at(kTraceK1 + blockIdx.x, 1);
+#endif
     const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
@@ -729,6 +756,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
         a.add(P, e, T_in, it, id, cs, cd, clane, cvs, cvd);
     }
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
+#ifdef PP_TRACE
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1))
+        trace_at(kTraceK1 + blockIdx.x, 2 + (threadIdx.x >> 6));
+#endif
 }
 
 // K1 for small batches: a group of G lanes per evaluation (G = 2 ... 16; kernels k_prep_g2 ... k_prep_g16), so that a batch of a few
@@ -1564,6 +1595,12 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     uint64_t* sAdj = (uint64_t*)(((uintptr_t)(sSlow + SPB) + 7) & ~(uintptr_t)7);
     int* sNg = (int*)(sAdj + 2 * SPB);
     if (tid < SPB) { sFlags[tid] = 0; sSlow[tid] = 0; }
+#ifdef PP_TRACE
+    if (!kSlow && tid == 0) {
+        PP_TRACE_AT(blockIdx.x, 0);
+        if (blockIdx.x < (unsigned)kTraceK1) g_trace[8 * blockIdx.x + 7] = trace_hwid();
+    }
+#endif
 #ifdef PP_CHECK
     for (int i = tid; i < 5 * nslot * kKP; i += (int)blockDim.x) sX[i] = __builtin_nan("");
     for (int i = tid; i < 4 * nslot; i += (int)blockDim.x) sMeta[i] = kMetaPoison;
@@ -1714,12 +1751,14 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         if (D > 1) flags |= (uint32_t)pv.status[v];     // every draw's planner flags
         atomicOr(&sFlags[sc_l], flags);
     }
+    if (!kSlow && (tid & 63) == 0 && tid < 256) PP_TRACE_AT(blockIdx.x, 2 + (tid >> 6));
     __syncthreads();
     if (tid < nsc && ((sSlow[tid] != 0) == kSlow) && PP_CHK(s0 + tid < g_lim.nscen, 15, s0 + tid)) {
         const uint32_t st = (uint32_t)pv.status[(s0 + tid) * D] | sFlags[tid];
         if (BPS == 1) out.status[s0 + tid] = st;
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
     }
+    if (!kSlow && tid == 0) PP_TRACE_AT(blockIdx.x, 6);
     if (kMode == 1 && emit_in) {
         // K4 in the block (reference mode): the spline slots are free now, so the team computes
         // the sin/cos of every recorded turn of the block's winners into them (one item per
@@ -2660,6 +2699,14 @@ int32_t pp_check_read(unsigned long long* out, int32_t reset) {  // checking bui
         unsigned long long z[8] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, sizeof z) != hipSuccess) return -1;
     }
+    return 0;
+}
+#endif
+#ifdef PP_TRACE
+int32_t pp_trace_read(unsigned long long* out, int64_t words) {   // diagnostic builds only: g_trace
+    if (words > 8LL * kTraceMax) words = 8LL * kTraceMax;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), sizeof(unsigned long long) * words) != hipSuccess) return -1;
     return 0;
 }
 #endif
