@@ -1954,7 +1954,7 @@ __device__ __forceinline__ void emit_scene(const pp_scene_batch& in, const pp_pa
 #pragma unroll
             for (int u = 0; u < kChunk; u++) turn_sincos<false>(rt[u], srs[u], crs[u]);
         }
-#pragma unroll
+        // (not unrolled: the exits keep the compiler from it, as in emit_scene_rows below)
         for (int u = 0; u < kChunk; u++) {
             const int g = g0 + u;
             if (g >= ng) break;
@@ -2048,7 +2048,9 @@ __device__ __forceinline__ void emit_scene_rows(const pp_scene_batch& in, const 
 #pragma unroll
             for (int u = 0; u < kChunk; u++) turn_sincos<false>(rt[u], srs[u], crs[u]);
         }
-#pragma unroll
+        // (a loop, not unrolled: its two exits keep the compiler from unrolling it, and the
+        // unrolled form, written with guards instead of exits, measured 4 % slower: k_emit 0.79 ->
+        // 0.82 ms at config 5, profiles/r04_ablations.txt)
         for (int u = 0; u < kChunk; u++) {
             const int i = i0 + u;
             if (i >= N) break;
@@ -2111,6 +2113,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int n = mg.n;
+#ifdef PP_TRACE
+    // (block 0: start, after K1, after the fast scenes' K2 + K4, end; words at group kTraceK1 - 1)
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 0);
+#endif
     for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) sm[i] = mg.buf[i];
     __syncthreads();
     const MapV m = map_view(sm, n, mg.fastm);
@@ -2122,11 +2128,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         if (q < SPB && v < in.n_scenes) prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, v, (int)threadIdx.x % 16);
     }
     __syncthreads();
+#ifdef PP_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 1);
+#endif
     const MapG ml = {sm, n, mg.fastm};
     double* csm = sm + ((kMapArrays * n + 1) & ~1);
     cand_group<false, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
     __syncthreads();
+#ifdef PP_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 2);
+#endif
     cand_group<true, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
+#ifdef PP_TRACE
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 3);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2326,6 +2341,8 @@ struct StreamWS {
     int64_t rec_cap = 0;
     uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
     int64_t gbits_cap = 0;        // words
+    hipStream_t st2 = nullptr;    // the two-stream split's second stream (shard-sized batches)
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 struct DevState {
     bool init = false;
@@ -2530,6 +2547,16 @@ bool fused_small(int64_t S) {
     return f ? f != PP_SHAPE_SPLIT : S <= kFusedSmall;
 }
 bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
+// Two-stream split (reference mode, no paths): batches of about one 8-GPU shard of BASELINE config 5
+// (262,144 scenes) run as two halves, each K1 -> K2 -> K4 on its own stream, so one half's kernels
+// fill the other's start-up and tail (a batch this size is ~15 rounds of k_cand blocks and one of
+// k_prep waves). PP_DBG_SPLIT 1 forces it (any split-eligible batch), 2 off.
+constexpr int64_t kSplitMin = 131072, kSplitMax = 786432;
+bool split_on(int64_t S) {
+    const int f = dbg(PP_DBG_SPLIT);
+    if (f == 2) return false;
+    return f == 1 ? S >= 2048 : (S >= kSplitMin && S <= kSplitMax);
+}
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
 // 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
 // scenes: 2.07 ms for 32,768 waves at 3, 2.29 ms at 4); 262,144 scenes (BASELINE config 5 over 8
@@ -2608,7 +2635,8 @@ int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     if (W.gbits_cap >= words) return PP_OK;
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
-    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 1 + 32 * cap);
+    // [bits: cap words][flagged-group count][the split's second-half count][list: 32 cap entries]
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 2 + 32 * cap);
     if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
@@ -2616,6 +2644,9 @@ int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
 }
 
 void free_ws(StreamWS& W) {
+    if (W.st2) (void)hipStreamDestroy(W.st2);
+    if (W.fork) (void)hipEventDestroy(W.fork);
+    if (W.join) (void)hipEventDestroy(W.join);
     if (W.ws) (void)hipFree(W.ws);
     if (W.rec) (void)hipFree(W.rec);
     if (W.gbits) (void)hipFree(W.gbits);
@@ -2910,7 +2941,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             if (w) return PP_ERR_STATE;
         const bool ok = fill(W.ws, prep_bytes(W.ws_cap)) &&
                         fill(W.rec, W.rec ? rec_bytes(W.rec_cap) : 0) &&
-                        fill(W.gbits + W.gbits_cap + 1, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
+                        fill(W.gbits + W.gbits_cap + 2, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
                         fill(out->winner, 4 * S) && fill(out->n_out, 4 * S) && fill(out->status, 4 * S) &&
                         fill(out->next_x, 8 * N * S) && fill(out->next_y, 8 * N * S) &&
                         fill(out->cost, 8 * Cn * S) && fill(out->info, sizeof(pp_scene_info) * S) &&
@@ -2946,7 +2977,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     gb.count = W.gbits + W.gbits_cap;
-    gb.list = gb.count + 1;
+    gb.list = gb.count + 2;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -2977,7 +3008,58 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
-    if (hipMemsetAsync(gb.count, 0, sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
+    if (hipMemsetAsync(gb.count, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
+    const bool split = ref_direct && !P.emit_paths && !fused && cg.bps == 1 && Dn == 1 &&
+                       prep_group(Sv) == 1 && split_on(S);
+    if (split) {
+        // halves at a group boundary: groups [0, ga) (scenes [0, sa)) on the caller's stream,
+        // [ga, G) on the second; each half its own flagged-group list (count words 0 and 1, the
+        // second half's list after the first half's ga entries). The per-kernel events become
+        // phases: K1 of the first half, its K2, then the rest (both halves overlap in each).
+        if (!W.st2) {
+            if (hipStreamCreateWithFlags(&W.st2, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&W.join, hipEventDisableTiming) != hipSuccess)
+                return PP_ERR_HIP;
+        }
+        const int64_t G = cg.groups, ga = G / 2, sa = std::min<int64_t>(S, ga * cg.spb);
+        GroupBits gbh[2] = {gb, gb};
+        gbh[1].count = gb.count + 1;
+        gbh[1].list = gb.list + ga;
+        if (timing) (void)hipEventRecord(ev[0], st);
+        if (hipEventRecord(W.fork, st) != hipSuccess || hipStreamWaitEvent(W.st2, W.fork, 0) != hipSuccess)
+            return PP_ERR_HIP;
+        const bool lmap = mg.n <= kLdsMapMax;
+        const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
+        for (int h = 0; h < 2; h++) {
+            hipStream_t sh = h == 0 ? st : W.st2;
+            const int64_t v0 = h == 0 ? 0 : sa, v1 = h == 0 ? sa : S;
+            const int64_t g0 = h == 0 ? 0 : ga, g1 = h == 0 ? ga : G;
+            if (v1 <= v0) continue;
+            const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
+            if (prep_w4(v1 - v0, device)) {
+                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+            } else {
+                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+            }
+            if (timing && h == 0) (void)hipEventRecord(ev[1], st);
+            const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
+            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
+                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
+            hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
+                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
+            if (timing && h == 0) (void)hipEventRecord(ev[2], st);
+            hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
+                               rec, adjm, v0, v1);
+        }
+        if (hipEventRecord(W.join, W.st2) != hipSuccess || hipStreamWaitEvent(st, W.join, 0) != hipSuccess)
+            return PP_ERR_HIP;
+        if (timing) (void)hipEventRecord(ev[3], st);
+        if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
+        return PP_OK;
+    }
     // K1: one lane per evaluation, or a group of G lanes per evaluation for small batches
     {
         const int threads = 256;
@@ -3056,6 +3138,7 @@ int32_t pp_debug_set(int32_t key, int32_t value) {
         case PP_DBG_PREP_WAVES: ok = value == 0 || value == 3 || value == 4; break;
         case PP_DBG_SHAPE: ok = value >= 0 && value <= PP_SHAPE_STEP; break;
         case PP_DBG_POISON: ok = value == 0 || value == 1; break;
+        case PP_DBG_SPLIT: ok = value >= 0 && value <= 2; break;
         default: break;
     }
     if (!ok) return PP_ERR_ARG;

@@ -548,7 +548,8 @@ DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
 
 
 # pp_debug_set keys and launch shapes (include/pp.h PP_DBG_*, PP_SHAPE_*)
-DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON = 0, 1, 2, 3
+DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT = 0, 1, 2, 3, 4
+SPLIT_AUTO, SPLIT_ON, SPLIT_OFF = 0, 1, 2
 SHAPE_AUTO, SHAPE_SPLIT, SHAPE_CAND_SMALL, SHAPE_STEP = 0, 1, 2, 3
 
 
