@@ -108,6 +108,16 @@ def load_pmc_all():
         return {}
 
 
+def load_rocprof_all():
+    """The committed rocprofv3 kernel-trace summary (profiles/rocprof_summary.json, written by
+    tools/rocprof_summarize.py): per launch-shape tag, the profiler's average K2 launch duration."""
+    p = os.path.join(REPO, "profiles", "rocprof_summary.json")
+    try:
+        return json.load(open(p))
+    except Exception:
+        return {}
+
+
 def pmc_tag(S, Cn, N, emit_paths, D):
     return f"k_cand_S{S}_C{Cn}_N{N}" + ("_paths" if emit_paths else "") + (f"_D{D}" if D > 1 else "")
 
@@ -582,10 +592,17 @@ def main(argv=None):
     # dominant kernel: k_cand on this rank
     k_cand_ms = kms["k_cand"]
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
-    cands_launch = S * Cn
+    # K2 launches per step: 2 where pp_eval splits the batch over two streams (shard sizes), each
+    # launch timed on its own stream and covering half the candidates
+    k2_per_step = max(launches[1] // max(a.steps * frames, 1), 1)
+    cands_launch = S * Cn // k2_per_step
     achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
     pmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D)
     traffic, traffic_pipe = roofline_fields(pmc, cands_launch, bpc, k_cand_ms)
+    # the same fraction from the profiler's average K2 duration of this exact launch shape (a
+    # committed rocprofv3 run of this command; durations do not carry over between batch sizes)
+    rp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D))
+    rp = rp if rp and rp.get("launches_per_step") == k2_per_step else None
     wname = workload_name(S, Cn, a.n_speeds, a.n_points, a.emit_paths, D, a.rollout)
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",
@@ -611,6 +628,12 @@ def main(argv=None):
         "per_rank_kernels_ms": per_rank,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": k_cand_ms, "launches_per_step": k2_per_step,
+                     "kernel_time_source": "HIP events on each K2 launch's own stream, timed region",
+                     "frac_rocprof": (bpc * cands_launch / (rp["dominant_ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                      if rp else None),
+                     "kernel_ms_rocprof": rp["dominant_ms_per_launch"] if rp else None,
+                     "rocprof_source": rp["source"] if rp else None,
                      "kernel": ", ".join(pmc["kernels"]) if pmc and pmc.get("kernels") else "k_cand",
                      "algorithmic_bytes_per_candidate": bpc,
                      "traffic_pipeline": traffic_pipe,

@@ -15,6 +15,7 @@
 //                each block runs the winners and writes next_x/next_y)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
@@ -86,8 +87,11 @@ __device__ __forceinline__ unsigned long long trace_hwid() {
     return ((unsigned long long)xcc << 32) | hw;
 }
 #define PP_TRACE_AT(blk, k) do { if ((blk) < (unsigned)kTraceK1) trace_at((blk), (k)); } while (0)
+// the grouped K1 of block 0 (k_step_small's single frame), lane 0: words at group kTraceK1 - 2
+#define PP_TRACE_K1(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 2, (k)); } while (0)
 #else
 #define PP_TRACE_AT(blk, k) ((void)0)
+#define PP_TRACE_K1(k) ((void)0)
 #endif
 #include "pp_device.h"
 #include "pp_glibcm.h"
@@ -266,6 +270,28 @@ __device__ __forceinline__ void rec_ld(const double* rec, int64_t rstride, int64
     double* r = (double*)rec;
     x = PP_LD(rec_px(r, rstride, g, S, s));
     y = PP_LD(rec_py(r, rstride, g, S, s));
+}
+// The map into LDS (16-B aligned both sides): 16-B loads, each thread's loads issued before its LDS
+// stores, so a block stages a map of up to 8 x 512 doubles (highway_map.csv: 3,439) in one round
+// trip to memory instead of one per element (the single-frame kernel waits for it)
+__device__ __forceinline__ void stage_map(double* __restrict__ dst, const double* __restrict__ src, int nd) {
+    typedef double dv2 __attribute__((ext_vector_type(2)));
+    constexpr int kU = 8;
+    const int n2 = nd / 2;
+    for (int i0 = threadIdx.x; i0 < n2; i0 += kU * blockDim.x) {
+        dv2 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * (int)blockDim.x;
+            if (i < n2) v[u] = ((const dv2*)src)[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int i = i0 + u * (int)blockDim.x;
+            if (i < n2) ((dv2*)dst)[i] = v[u];
+        }
+    }
+    if ((nd & 1) && threadIdx.x == 0) dst[nd - 1] = src[nd - 1];
 }
 // kLdsMap: the map (kMapArrays n doubles) is staged in LDS (n <= kLdsMapMax: <= 62.4 KB, 600
 // waypoints at three lanes); larger maps are read from global memory (L2-resident) by the same code.
@@ -640,7 +666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     }
 #endif
     if (kLdsMap) {
-        for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
+        stage_map(smap, mg.buf, kMapArrays * n);
         __syncthreads();
     }
 #ifdef PP_TRACE
@@ -779,7 +805,7 @@ __device__ __forceinline__ void prep_grp_body(MapG mg, pp_scene_batch in, pp_par
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
     if (kLdsMap) {
-        for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) smap[i] = mg.buf[i];
+        stage_map(smap, mg.buf, kMapArrays * n);
         __syncthreads();
     }
     const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
@@ -802,7 +828,9 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
     const int draw = (int)(v - s * D);
 
     EgoSt e;
+    PP_TRACE_K1(0);
     prep_ego<G>(m, in, P, S, s, r, e);
+    PP_TRACE_K1(1);
     uint32_t status = e.status;
     const int T_in = in.prev_target_lane[s];
     PlanAcc a;
@@ -820,28 +848,66 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
         const int j = j0 + r;
         int okl = 0, id = 0;                  // okl: matched | lane << 1
         double cs = 0, cd = 0, cvs = 0, cvd = 0;
+        // table mode: slot j holds id sid; its reported row, if any (rows ascend by id: the first
+        // row with that id, the row k_prep's merge pointer reaches). Slot ids ascend strictly; a
+        // slot repeating its predecessor's id is padding (pp_cartable.h pads with INT32_MAX, which
+        // may also be a real car's id): it matches no row, as k_prep's merge pointer has already
+        // passed that row. The group's lanes load the rows' ids (row p0 + q in lane q) and every
+        // lane scans them by shuffles: one round trip to memory for the ids, not one per row
+        // visited (the single-frame kernel waits for every one of those).
+        int trow = -1, sid = 0;
+        // (frames of at most G rows: the rows' cars come along with their ids, and the found row's
+        // by a shuffle; the slot's stored state is read with its id: no load waits on the search)
+        double fx = 0, fy = 0, fvx = 0, fvy = 0;
+        bool fgot = false;
+        int sv = 0, sln = 0;
+        double ss = 0, sd = 0, svs = 0, svd = 0;
+        if (tab) {
+            const bool live = j < iters;
+            const int64_t tix = (int64_t)j * S + s;
+            sid = live ? (in.tab_id ? in.tab_id[tix] : j) : 0;
+            if (live) {
+                sv = in.tab_valid[tix]; sln = in.tab_lane[tix];
+                ss = in.tab_s[tix]; sd = in.tab_d[tix]; svs = in.tab_vs[tix]; svd = in.tab_vd[tix];
+            }
+            bool done = !live || (in.tab_id && j > 0 && in.tab_id[tix - S] >= sid);
+            for (int p0 = 0; p0 < ncar; p0 += G) {
+                const int pl = p0 + r;
+                int pid = 0;
+                double px = 0, py = 0, pvx = 0, pvy = 0;
+                if (pl < ncar) {
+                    const int64_t ix = (int64_t)pl * S + s;
+                    pid = in.car_id[ix];
+                    if (ncar <= G) { px = in.car_x[ix]; py = in.car_y[ix]; pvx = in.car_vx[ix]; pvy = in.car_vy[ix]; }
+                }
+                const int nq = ncar - p0 < G ? ncar - p0 : G;
+                for (int q = 0; q < nq; q++) {
+                    const int cid = __shfl(pid, q, G);
+                    if (!done && cid >= sid) { if (cid == sid) trow = p0 + q; done = true; }
+                }
+                if (ncar <= G) {              // (group-uniform)
+                    const int src = trow >= 0 ? trow : 0;
+                    fx = __shfl(px, src, G); fy = __shfl(py, src, G);
+                    fvx = __shfl(pvx, src, G); fvy = __shfl(pvy, src, G);
+                    fgot = trow >= 0;
+                }
+                if (grp_or<G>(done ? 0u : 1u) == 0u) break;
+            }
+        }
+        PP_TRACE_K1(2);
         if (j < iters) {
             const int64_t tix = (int64_t)j * S + s;
             int row = j;
-            if (tab) {
-                // slot j holds id sid; its reported row, if any (rows ascend by id: the first row
-                // with that id, the row k_prep's merge pointer reaches)
-                const int sid = in.tab_id ? in.tab_id[tix] : j;
-                row = -1;
-                // slot ids ascend strictly; a slot repeating its predecessor's id is padding
-                // (pp_cartable.h pads with INT32_MAX, which may also be a real car's id): it
-                // matches no row, as k_prep's merge pointer has already passed that row
-                const bool pad = in.tab_id && j > 0 && in.tab_id[tix - S] >= sid;
-                for (int p = pad ? ncar : 0; p < ncar; p++) {
-                    const int cid = in.car_id[(int64_t)p * S + s];
-                    if (cid >= sid) { if (cid == sid) row = p; break; }
-                }
-                id = sid;
-            }
+            if (tab) { row = trow; id = sid; }
             if (row >= 0) {
                 const int64_t ix = (int64_t)row * S + s;
-                id = in.car_id[ix];
-                double cx = in.car_x[ix], cy = in.car_y[ix], cvx = in.car_vx[ix], cvy = in.car_vy[ix];
+                double cx, cy, cvx, cvy;
+                if (fgot) {                   // (tab: the row's id is the slot's)
+                    cx = fx; cy = fy; cvx = fvx; cvy = fvy;
+                } else {
+                    id = in.car_id[ix];
+                    cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
+                }
                 if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
                 int nwp = 0, clane = 0;
                 if (lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
@@ -856,11 +922,12 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
                     ust |= PP_ST_CAR_UNMATCHED;
                     if (tab) in.tab_valid[tix] = 0;
                 }
-            } else if (in.tab_valid[tix]) {   // (tab only) a stale slot
-                okl = 1 | (in.tab_lane[tix] << 1);
-                cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
+            } else if (sv) {                  // (tab only) a stale slot
+                okl = 1 | (sln << 1);
+                cs = ss; cd = sd; cvs = svs; cvd = svd;
             }
         }
+        PP_TRACE_K1(3);
         const int nq = iters - j0 < G ? iters - j0 : G;
         for (int q = 0; q < nq; q++) {
             const int qokl = __shfl(okl, q, G);
@@ -870,11 +937,13 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
             if (qokl & 1) a.add(P, e, T_in, j0 + q, qid, qcs, qcd, qokl >> 1, qcvs, qcvd);
         }
     }
+    PP_TRACE_K1(4);
     status |= grp_or<G>(ust);
     // prep_finish re-reads the follow cars' velocities from the slots other lanes of the group
     // (same wave) wrote above
     if (tab) __threadfence_block();
     prep_finish<G>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, r, T_in, e, a, status);
+    PP_TRACE_K1(5);
 }
 
 // the grouped instantiations by name (pp_eval's launch switch)
@@ -1645,6 +1714,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         if (act) team_a5(sl, r, TS);
     }
     __syncthreads();
+    if (!kSlow && tid == 0) PP_TRACE_AT(blockIdx.x, 1);
     // Lane -> candidate. Reference mode without draws (kMode 1): lanes [0, nsc) run the scenes'
     // winning candidates (planner lane T, max_speed: known from k_prep) and record their paths;
     // lanes >= nsc run the C - 1 other candidates of each scene cost-only. The output work is
@@ -1780,6 +1850,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             pcr[idx] = cr; psr[idx] = sr;
         }
         __syncthreads();
+        if (!kSlow && tid == 0) PP_TRACE_AT(blockIdx.x, 7);
         if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
             const int64_t s = s0 + tid;
             emit_scene_pre<kEmitChunk>(in, P, pv, out, rec, s, pv.K[s], sNg[tid], sAdj[2 * tid],
@@ -2108,16 +2179,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // phase A reading the same LDS map. The prep record goes through global memory inside the block
 // (written, barrier, read by the same workgroup). No kernel boundary is left in the step.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small(
-        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
-        uint64_t* adjm) {
+__device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
+                                                const PrepV& pv, const pp_result& out, int SPB, double* rec,
+                                                uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int n = mg.n;
 #ifdef PP_TRACE
     // (block 0: start, after K1, after the fast scenes' K2 + K4, end; words at group kTraceK1 - 1)
     if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 0);
 #endif
-    for (int i = threadIdx.x; i < kMapArrays * n; i += blockDim.x) sm[i] = mg.buf[i];
+    stage_map(sm, mg.buf, kMapArrays * n);
     __syncthreads();
     const MapV m = map_view(sm, n, mg.fastm);
     const int64_t g = blockIdx.x;
@@ -2142,6 +2213,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #ifdef PP_TRACE
     if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 3);
 #endif
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm) {
+    step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+}
+
+// ------------------------------------------------------------------------------------------------
+// pp_plan_frame in one launch: the frame's input ranges are read from pinned host memory into the
+// device frame by the block itself, k_step_small's body runs, the output ranges are written back
+// to pinned host memory, and a sequence number in host memory tells the waiting host thread the
+// frame is done — no copy commands and no stream synchronisation per frame.
+// Ranges are 4-byte-word ranges of the frame (host and device share the layout).
+// ------------------------------------------------------------------------------------------------
+constexpr int kFioMax = 16;
+struct FrameIO {
+    const uint32_t* h_in;     // pinned host frame (inputs)
+    uint32_t* d_frame;        // device frame
+    uint32_t* h_out;          // pinned host frame (outputs)
+    uint32_t* h_flag;         // pinned host word: seq once the outputs are in place
+    uint32_t seq;
+    int n_in, n_out;
+    uint32_t in_off[kFioMax], in_len[kFioMax], out_off[kFioMax], out_len[kFioMax];   // words
+};
+// words [0, total) of the ranges, thread t taking t, t + blockDim.x, ...: every thread's loads are
+// issued before its stores (one round trip to the host per kChunk words)
+template <int kChunk>
+__device__ __forceinline__ void frame_copy(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                           int nr, const uint32_t* off, const uint32_t* len) {
+    uint32_t total = 0;
+    for (int r = 0; r < nr; r++) total += len[r];
+    for (uint32_t w0 = threadIdx.x; w0 < total; w0 += kChunk * blockDim.x) {
+        uint32_t v[kChunk], at[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {
+            uint32_t w = w0 + u * blockDim.x;
+            at[u] = 0xffffffffu;
+            if (w < total) {
+                int r = 0;
+                while (w >= len[r]) { w -= len[r]; r++; }
+                at[u] = off[r] + w;
+                v[u] = __builtin_nontemporal_load(src + at[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kChunk; u++)
+            if (at[u] != 0xffffffffu) dst[at[u]] = v[u];
+    }
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_plan_frame(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm, FrameIO io) {
+    frame_copy<8>(io.h_in, io.d_frame, io.n_in, io.in_off, io.in_len);
+    __threadfence_block();
+    __syncthreads();
+    step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+    __threadfence_block();
+    __syncthreads();
+    frame_copy<8>(io.d_frame, io.h_out, io.n_out, io.out_off, io.out_len);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(io.h_flag, io.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2350,8 +2483,10 @@ struct DevState {
     double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
-    void* frame_host = nullptr;   // its pinned host staging copy
-    hipStream_t frame_stream = nullptr;  // pp_plan_frame's stream (copies and kernels, one sync)
+    void* frame_host = nullptr;   // its pinned host staging copy (coherent: k_plan_frame reads and
+                                  // writes it; the frame's done word follows the frame)
+    hipStream_t frame_stream = nullptr;  // pp_plan_frame's stream
+    uint32_t frame_seq = 0;       // the last frame's done word
     std::mutex frame_mu;          // one pp_plan_frame at a time per device (frame scratch + car table)
     void* stage = nullptr;        // pp_plan_batch_host staging buffer
     size_t stage_cap = 0;
@@ -2360,8 +2495,10 @@ struct DevState {
     pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
     bool timing = false;          // pp_timing_enable
     std::vector<hipEvent_t> ev_pool;
-    std::vector<hipEvent_t> ev_rec; // groups of 4: before k_prep, after k_prep, after k_cand, after k_winner
-    std::vector<int> ev_has3;     // per group: k_winner launched
+    // groups of 8 per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch stream (the
+    // two-stream split: those four per half, each half's on its own stream, events 4-7 the second's)
+    std::vector<hipEvent_t> ev_rec;
+    std::vector<int> ev_kind;     // per group: bit 0 K3/K4 launched, bit 1 two-stream split
 };
 
 }  // namespace
@@ -2874,8 +3011,12 @@ int32_t pp_reserve(pp_map* M, int32_t device, int64_t max_scenes) {
     return ensure_rec(W, nullptr, max_scenes);
 }
 
-int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
-                int32_t device, void* hip_stream) {
+}  // extern "C"
+namespace {
+// pp_eval; fio (pp_plan_frame): the single-launch frame kernel with host-memory staging, where the
+// call takes the fused one-launch shape (PP_ERR_STATE otherwise: the caller stages by copies)
+int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
+                  int32_t device, void* hip_stream, const FrameIO* fio) {
     if (!M || !in || !out || !params_ok(prm) || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
     if (in->n_scenes < 0 || in->car_stride < 0 || in->car_stride > PP_MAX_CARS) return PP_ERR_ARG;
     if (in->n_scenes == 0) return PP_OK;
@@ -2907,6 +3048,13 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     const bool fused = ref_direct && !prm->emit_paths && cg.bps == 1 && emit_in_ok(prm->n_points) &&
                        fused_small(S);
     const bool emit_in = fused;
+    // small reference-mode batches with the map in LDS: the whole step in one launch (k_step_small)
+    const int spb_f = std::min(cg.spb, 256 / 16);
+    const int64_t groups_f = (S + spb_f - 1) / spb_f;
+    const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * M->n + 1) & ~1);
+    const size_t lds_f = map_lds + cand_geom_lds(spb_f);
+    const bool step_fused = fused && M->n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
+    if (fio && (!step_fused || groups_f != 1)) return PP_ERR_STATE;
     // the map lock is held from workspace binding through the (asynchronous) launches: a
     // concurrent call cannot grow and free this stream's buffers in between
     std::lock_guard<std::mutex> lk(M->mu);
@@ -2955,10 +3103,10 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     mg.buf = DS.map;
     mg.n = M->n;
     mg.fastm = M->fastm;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev[8] = {};
     const bool timing = DS.timing;
     if (timing) {
-        for (int i = 0; i < 4; i++) {
+        for (int i = 0; i < 8; i++) {
             if (DS.ev_pool.empty()) {
                 hipEvent_t e;
                 if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
@@ -2968,7 +3116,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             DS.ev_pool.pop_back();
             DS.ev_rec.push_back(ev[i]);
         }
-        DS.ev_has3.push_back(!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0);
+        DS.ev_kind.push_back(!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0);
     }
     pp_params P = *prm;
     pp_scene_batch B = *in;
@@ -2991,19 +3139,18 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             hipMemcpyToSymbol(HIP_SYMBOL(g_lim), &L, sizeof L) != hipSuccess) return PP_ERR_HIP;
     }
 #endif
-    // small reference-mode batches with the map in LDS: the whole step in one launch (k_step_small)
-    const int spb_f = std::min(cg.spb, 256 / 16);
-    const int64_t groups_f = (S + spb_f - 1) / spb_f;
-    const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * mg.n + 1) & ~1);
-    const size_t lds_f = map_lds + cand_geom_lds(spb_f);
-    const bool step_fused = fused && mg.n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
     if (step_fused) {
         if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
         // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
         const int threads_f = std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
-        hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
-                           R, spb_f, rec, adjm);
+        if (fio) {
+            hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, mg, B, P, pv, R, spb_f, rec,
+                               adjm, *fio);
+        } else {
+            hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
+                               R, spb_f, rec, adjm);
+        }
         if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
@@ -3014,8 +3161,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     if (split) {
         // halves at a group boundary: groups [0, ga) (scenes [0, sa)) on the caller's stream,
         // [ga, G) on the second; each half its own flagged-group list (count words 0 and 1, the
-        // second half's list after the first half's ga entries). The per-kernel events become
-        // phases: K1 of the first half, its K2, then the rest (both halves overlap in each).
+        // second half's list after the first half's ga entries). Timing: each half's kernels by
+        // events on its own stream (two launches of each kernel per call; they overlap the other
+        // half's, as in a rocprofv3 kernel trace of the same call).
         if (!W.st2) {
             if (hipStreamCreateWithFlags(&W.st2, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess ||
@@ -3026,7 +3174,7 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
         GroupBits gbh[2] = {gb, gb};
         gbh[1].count = gb.count + 1;
         gbh[1].list = gb.list + ga;
-        if (timing) (void)hipEventRecord(ev[0], st);
+        if (timing) DS.ev_kind.back() |= 2;
         if (hipEventRecord(W.fork, st) != hipSuccess || hipStreamWaitEvent(W.st2, W.fork, 0) != hipSuccess)
             return PP_ERR_HIP;
         const bool lmap = mg.n <= kLdsMapMax;
@@ -3035,7 +3183,9 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
             hipStream_t sh = h == 0 ? st : W.st2;
             const int64_t v0 = h == 0 ? 0 : sa, v1 = h == 0 ? sa : S;
             const int64_t g0 = h == 0 ? 0 : ga, g1 = h == 0 ? ga : G;
-            if (v1 <= v0) continue;
+            if (v1 <= v0) continue;     // (never: the split takes batches of >= 2,048 scenes)
+            hipEvent_t* eh = ev + 4 * h;
+            if (timing) (void)hipEventRecord(eh[0], sh);
             const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
             if (prep_w4(v1 - v0, device)) {
                 if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
@@ -3044,19 +3194,19 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
                 if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
                 else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
             }
-            if (timing && h == 0) (void)hipEventRecord(ev[1], st);
+            if (timing) (void)hipEventRecord(eh[1], sh);
             const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
             hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
             hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
-            if (timing && h == 0) (void)hipEventRecord(ev[2], st);
+            if (timing) (void)hipEventRecord(eh[2], sh);
             hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
                                rec, adjm, v0, v1);
+            if (timing) (void)hipEventRecord(eh[3], sh);
         }
         if (hipEventRecord(W.join, W.st2) != hipSuccess || hipStreamWaitEvent(st, W.join, 0) != hipSuccess)
             return PP_ERR_HIP;
-        if (timing) (void)hipEventRecord(ev[3], st);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
@@ -3131,6 +3281,14 @@ int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_re
     return PP_OK;
 }
 
+}  // namespace
+extern "C" {
+
+int32_t pp_eval(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_result* out,
+                int32_t device, void* hip_stream) {
+    return eval_impl(M, in, prm, out, device, hip_stream, nullptr);
+}
+
 int32_t pp_debug_set(int32_t key, int32_t value) {
     bool ok = false;
     switch (key) {
@@ -3162,20 +3320,23 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     DeviceGuard g(device);
     for (int k = 0; k < 3; k++) { ms3[k] = 0; launches3[k] = 0; }
     int rc = PP_OK;
-    const size_t ng = D.ev_rec.size() / 4;
+    const size_t ng = D.ev_rec.size() / 8;
     for (size_t i = 0; i < ng; i++) {
-        hipEvent_t* e = &D.ev_rec[4 * i];
-        if (hipEventSynchronize(e[3]) != hipSuccess) rc = PP_ERR_HIP;
-        float t;
-        if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
-        if (hipEventElapsedTime(&t, e[1], e[2]) == hipSuccess) { ms3[1] += t; launches3[1]++; } else rc = PP_ERR_HIP;
-        if (D.ev_has3[i]) {
-            if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
+        const int kind = D.ev_kind[i];
+        for (int h = 0; h < ((kind & 2) ? 2 : 1); h++) {
+            hipEvent_t* e = &D.ev_rec[8 * i + 4 * h];
+            if (hipEventSynchronize(e[3]) != hipSuccess) rc = PP_ERR_HIP;
+            float t;
+            if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
+            if (hipEventElapsedTime(&t, e[1], e[2]) == hipSuccess) { ms3[1] += t; launches3[1]++; } else rc = PP_ERR_HIP;
+            if (kind & 1) {
+                if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
+            }
         }
-        for (int k = 0; k < 4; k++) D.ev_pool.push_back(e[k]);
+        for (int k = 0; k < 8; k++) D.ev_pool.push_back(D.ev_rec[8 * i + k]);
     }
     D.ev_rec.clear();
-    D.ev_has3.clear();
+    D.ev_kind.clear();
     return rc;
 }
 
@@ -3489,18 +3650,24 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     std::lock_guard<std::mutex> frame_lock(M->dev[device].frame_mu);
     DevState& DS = M->dev[device];
     Frame* d = nullptr;
+    constexpr size_t kFlagOff = (sizeof(Frame) + 63) / 64 * 64;
     {   // per-device scratch, made once: the device frame, its pinned host copy, the frame stream
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
         if (rc) return rc;
         if (!DS.frame && hipMalloc(&DS.frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
-        if (!DS.frame_host && hipHostMalloc(&DS.frame_host, sizeof(Frame), hipHostMallocDefault) != hipSuccess)
-            return PP_ERR_NOMEM;
+        if (!DS.frame_host) {
+            if (hipHostMalloc(&DS.frame_host, kFlagOff + 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                return PP_ERR_NOMEM;
+            memset(DS.frame_host, 0, kFlagOff + 64);
+            DS.frame_seq = 0;
+        }
         if (!DS.frame_stream && hipStreamCreateWithFlags(&DS.frame_stream, hipStreamNonBlocking) != hipSuccess)
             return PP_ERR_HIP;
         d = (Frame*)DS.frame;
     }
     Frame& h = *(Frame*)DS.frame_host;
+    volatile uint32_t* flag = (volatile uint32_t*)((char*)DS.frame_host + kFlagOff);
     memset(&h, 0, sizeof(h));
     const bool poison = dbg(PP_DBG_POISON) != 0;
     if (poison) {     // the outputs' staging starts NaN-filled (pp_eval poisons them on the device too)
@@ -3519,7 +3686,6 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS, poison);
     if (nslots < 0) return PP_ERR_ARG;                  // more than PP_MAX_CARS distinct cars
     hipStream_t st = DS.frame_stream;
-    if (hipMemcpyAsync(d, &h, sizeof(Frame), hipMemcpyHostToDevice, st) != hipSuccess) return PP_ERR_HIP;
     pp_scene_batch B;
     memset(&B, 0, sizeof(B));
     B.n_scenes = 1; B.car_stride = PP_MAX_CARS;
@@ -3536,11 +3702,62 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     memset(&R, 0, sizeof(R));
     R.winner = &d->winner; R.n_out = &d->nout; R.next_x = d->nx; R.next_y = d->ny; R.cost = d->cost;
     R.status = &d->status; R.info = &d->info;
-    int rc = pp_eval(M, &B, &P, &R, device, (void*)st);
-    // one copy back (plan, car table, scene info) and one synchronisation of the frame's stream
-    if (rc == PP_OK && (hipMemcpyAsync(&h, d, sizeof(Frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                        hipStreamSynchronize(st) != hipSuccess))
-        rc = PP_ERR_HIP;
+    // The frame's words that carry data: inputs (ego, previous path, this frame's rows, the table's
+    // nslots slots) and outputs (plan, costs, winner / count / status / info, the slots again).
+    FrameIO io;
+    memset(&io, 0, sizeof(io));
+    auto add = [&](bool in, const void* p, size_t bytes) {
+        const uint32_t off = (uint32_t)(((const char*)p - (const char*)&h) / 4), len = (uint32_t)(bytes / 4);
+        if (!len) return;
+        int& n = in ? io.n_in : io.n_out;
+        (in ? io.in_off : io.out_off)[n] = off;
+        (in ? io.in_len : io.out_len)[n] = len;
+        n++;
+    };
+    const size_t ns = (size_t)nslots, ncs = (size_t)nc;
+    add(true, h.ego, sizeof h.ego + sizeof h.px + sizeof h.py);   // ego, px, py: adjacent
+    add(true, h.cx, 8 * ncs); add(true, h.cy, 8 * ncs); add(true, h.cvx, 8 * ncs); add(true, h.cvy, 8 * ncs);
+    add(true, h.ts, 8 * ns); add(true, h.td, 8 * ns); add(true, h.tvs, 8 * ns); add(true, h.tvd, 8 * ns);
+    add(true, h.tvx, 8 * ns); add(true, h.tvy, 8 * ns);
+    add(true, h.tid, 4 * ns); add(true, h.tvalid, 4 * ns); add(true, h.tlane, 4 * ns);
+    add(true, &h.nprev, 4 * (3 + ncs));                          // nprev, ptl, ncars, cid[nc]: adjacent
+    add(false, h.nx, sizeof h.nx + sizeof h.ny + sizeof h.cost);  // nx, ny, cost: adjacent
+    add(false, h.ts, 8 * ns); add(false, h.td, 8 * ns); add(false, h.tvs, 8 * ns); add(false, h.tvd, 8 * ns);
+    add(false, h.tvx, 8 * ns); add(false, h.tvy, 8 * ns);
+    add(false, h.tvalid, 4 * ns); add(false, h.tlane, 4 * ns);
+    add(false, &h.winner, (size_t)((const char*)(&h.info + 1) - (const char*)&h.winner));   // winner .. info
+    static_assert(offsetof(Frame, px) == offsetof(Frame, ego) + sizeof(double) * 4 &&
+                  offsetof(Frame, py) == offsetof(Frame, px) + sizeof(double) * PP_PREV_KEEP &&
+                  offsetof(Frame, ny) == offsetof(Frame, nx) + sizeof(double) * N &&
+                  offsetof(Frame, cost) == offsetof(Frame, ny) + sizeof(double) * N &&
+                  offsetof(Frame, cid) == offsetof(Frame, nprev) + 12 && sizeof(pp_scene_info) % 4 == 0,
+                  "adjacent frame fields");
+    void* hdev = nullptr;
+    if (hipHostGetDevicePointer(&hdev, DS.frame_host, 0) != hipSuccess) return PP_ERR_HIP;
+    io.h_in = (const uint32_t*)hdev; io.h_out = (uint32_t*)hdev; io.d_frame = (uint32_t*)d;
+    io.h_flag = (uint32_t*)((char*)hdev + kFlagOff);
+    io.seq = ++DS.frame_seq;
+    int rc = eval_impl(M, &B, &P, &R, device, (void*)st, &io);
+    if (rc == PP_OK) {
+        // the kernel's done word; the stream is polled now and then, so a failed launch or a fault
+        // ends the wait with an error
+        for (uint64_t spin = 1; *flag != io.seq; spin++) {
+            if ((spin & 1023) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipSuccess && *flag != io.seq) { rc = PP_ERR_HIP; break; }
+                if (e != hipSuccess && e != hipErrorNotReady) { rc = PP_ERR_HIP; break; }
+            }
+            __builtin_ia32_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else if (rc == PP_ERR_STATE) {
+        // a launch shape other than the one-launch step (debug shapes, maps beyond the LDS): copies
+        if (hipMemcpyAsync(d, &h, sizeof(Frame), hipMemcpyHostToDevice, st) != hipSuccess) return PP_ERR_HIP;
+        rc = eval_impl(M, &B, &P, &R, device, (void*)st, nullptr);
+        if (rc == PP_OK && (hipMemcpyAsync(&h, d, sizeof(Frame), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                            hipStreamSynchronize(st) != hipSuccess))
+            rc = PP_ERR_HIP;
+    }
     if (rc != PP_OK) return rc;
     DS.plan_table.take_back(hs, 0, nslots);
     *n_out = h.nout;

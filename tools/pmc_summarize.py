@@ -8,9 +8,10 @@ import csv
 import glob
 import json
 import os
-import re
 import sys
 from collections import defaultdict
+
+from shape_tags import DOMINANT, parse_tag
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 tag = sys.argv[2] if len(sys.argv) > 2 else None
@@ -26,19 +27,6 @@ for k, d in vals.items():
 print(json.dumps(summary, indent=1))
 
 
-def parse_tag(tag):
-    """Launch shape from a bench tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>]."""
-    m = re.match(r"k_cand_S(\d+)_C(\d+)_N(\d+)(_paths)?(?:_D(\d+))?$", tag)
-    if not m:
-        raise SystemExit(f"pmc_summarize: tag {tag!r} is not k_cand_S<S>_C<C>_N<N>[_paths][_D<D>]")
-    S, C, N = int(m.group(1)), int(m.group(2)), int(m.group(3))
-    return {"scenes": S, "candidates_per_scene": C, "n_points": N, "emit_paths": bool(m.group(4)),
-            "draws": int(m.group(5) or 1), "candidates_per_launch": S * C}
-
-
-# the dominant kernel of a step: k_cand (both instantiations); the small-batch shapes fuse it
-# into k_cand_small / k_step_small
-DOMINANT = ("k_cand<", "k_cand_small", "k_step_small")
 STEP_KERNELS = ("k_prep", "k_prep_g2", "k_prep_g4", "k_prep_g8", "k_prep_g16", "k_cand", "k_cand_small",
                 "k_step_small", "k_emit", "k_winner")
 if tag:

@@ -1,0 +1,17 @@
+"""bench.py's launch-shape tags and the dominant kernel of a step (shared by pmc_summarize.py and
+rocprof_summarize.py)."""
+import re
+
+# the dominant kernel of a step: k_cand (both instantiations); the small-batch shapes fuse it
+# into k_cand_small / k_step_small
+DOMINANT = ("k_cand<", "k_cand_small", "k_step_small")
+
+
+def parse_tag(tag):
+    """Launch shape from a bench tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>]."""
+    m = re.match(r"k_cand_S(\d+)_C(\d+)_N(\d+)(_paths)?(?:_D(\d+))?$", tag)
+    if not m:
+        raise SystemExit(f"tag {tag!r} is not k_cand_S<S>_C<C>_N<N>[_paths][_D<D>]")
+    S, C, N = int(m.group(1)), int(m.group(2)), int(m.group(3))
+    return {"scenes": S, "candidates_per_scene": C, "n_points": N, "emit_paths": bool(m.group(4)),
+            "draws": int(m.group(5) or 1), "candidates_per_launch": S * C}
