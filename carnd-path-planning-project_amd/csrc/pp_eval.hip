@@ -239,7 +239,10 @@ __device__ __forceinline__ double turn_angle_fast(double nc, double speed, doubl
     return nad - adiff;
 }
 // Tuning constants (each measured against its alternatives):
-constexpr int kEmitChunk = 4;      // emit_scene_pre (small batches): recorded steps loaded together per lane
+#ifndef PP_EMIT_CHUNK
+#define PP_EMIT_CHUNK 4
+#endif
+constexpr int kEmitChunk = PP_EMIT_CHUNK;   // emit_scene_pre (small batches): recorded steps loaded together per lane
 constexpr int kEmitRows = 8;       // k_emit (large batches, emit_scene_rows): output rows per load round
 constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
 constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
@@ -397,6 +400,28 @@ __device__ __forceinline__ void put(T (&a)[NL], int l, T x) {
 #pragma unroll
     for (int i = 0; i < NL; i++) a[i] = l == i ? x : a[i];
 }
+// OR / sum over the G lanes of a group; (key, index) minimum with ties to the lower index
+template <int G>
+__device__ __forceinline__ uint32_t grp_or(uint32_t x) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o, G);
+    return x;
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_sum(uint32_t x) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, G);
+    return x;
+}
+template <int G>
+__device__ __forceinline__ void grp_argmin(double& key, int& idx) {
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        const double ok = __shfl_xor(key, o, G);
+        const int oi = __shfl_xor(idx, o, G);
+        if (ok < key || (ok == key && oi < idx)) { key = ok; idx = oi; }
+    }
+}
 struct PlanAcc {
     int lane_speed[NL];                     // the int-truncated lane speed where bit l of ls_set
     int ls_set;                             // (else P.max_speed)
@@ -440,16 +465,7 @@ struct PlanAcc {
             if (sp < ns || (sp == ns && ns != 1000 && it < it_of(clane))) {
                 put(next_s, clane, sp);
                 set_it(clane, it);
-                if (sp - ego_s < 200) {
-                    int speed = (int)cvs;
-                    if (speed > P.max_speed) speed = (int)P.max_speed;
-                    if (sp - ego_s > 100)
-                        speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
-                    put(lane_speed, clane, speed);
-                    ls_set |= 1 << clane;
-                } else {
-                    ls_set &= ~(1 << clane);
-                }
+                set_speed(P, ego_s, clane, sp, cvs);
             }
         }
         bool open = true;
@@ -490,14 +506,144 @@ struct PlanAcc {
             }
         }
     }
+    // the lane's speed where car (sp, cvs) holds next_s of its lane (src/main.cpp:385-399)
+    __device__ __forceinline__ void set_speed(const pp_params& P, double ego_s, int l, double sp, double cvs) {
+        if (sp - ego_s < 200) {
+            int speed = (int)cvs;
+            if (speed > P.max_speed) speed = (int)P.max_speed;
+            if (sp - ego_s > 100)
+                speed = (int)(speed + (P.max_speed - speed) * (sp - ego_s - 100) / (200.0 - 100.0));
+            put(lane_speed, l, speed);
+            ls_set |= 1 << l;
+        } else {
+            ls_set &= ~(1 << l);
+        }
+    }
+    // G cars at once, one per lane of the group (car it = this lane's iteration index; valid: a
+    // matched car), all with iteration indices above every car added before: the same state as
+    // add() over them in iteration order. Every selection is a minimum of (key, iteration index),
+    // reduced over the group by shuffles and merged into the running one by add()'s own rule; the
+    // per-car terms (planner keys, lane_open) are computed by each lane for its own car. The
+    // caller keeps add() for groups holding a car whose id is the 'no car' sentinel -1, which
+    // add() lets any later car replace.
+    template <int G>
+    __device__ __forceinline__ void add_group(const pp_params& P, const EgoSt& e, int T_in, bool valid, int it,
+                                              int id, double cs, double cd, int clane, double cvs, double cvd) {
+        const double ego_s = e.ego_s, ego_vs = e.ego_vs, dt0 = e.dt0;
+        const double kInf = __builtin_inf();
+        constexpr int kNone = 0x7fffffff;
+        nmatched += (int)grp_sum<G>(valid ? 1u : 0u);
+        const double sp = cs + cvs * dt0;
+        // next_s per lane: the first car with the smallest sp in (ego_s, 1000)
+#pragma unroll
+        for (int l = 0; l < NL; l++) {
+            double k = valid && clane == l && sp > ego_s && sp < 1000 ? sp : kInf;
+            int ki = k == kInf ? kNone : it;
+            grp_argmin<G>(k, ki);
+            const double wcvs = __shfl(cvs, ki == kNone ? 0 : ki - (it - (int)(threadIdx.x % G)), G);
+            const double ns = sel(next_s, l);
+            if (ki != kNone && (k < ns || (k == ns && ns != 1000 && ki < it_of(l)))) {
+                put(next_s, l, k);
+                set_it(l, ki);
+                set_speed(P, ego_s, l, k, wcvs);
+            }
+        }
+        // lane_open (src/main.cpp:401-444): a lane closes if any of its cars closes it
+        bool open = true;
+        {
+            double add = 2;
+            if (T_in == clane) add = 0;
+            const double min_dist = P.car_length + P.safety_distance + add;
+            if (fabs(ego_s - sp) < min_dist) open = false;
+            if (sp > ego_s && cvs < ego_vs) {
+                const double car_dist = sp - ego_s - P.car_length - P.safety_distance - add;
+                const double sd = ego_vs - cvs;
+                const double dtm = sd / P.relaxed_acc;
+                const double ddist = ego_vs * dtm - sd / 2 * dtm;
+                if (car_dist < ddist) open = false;
+            }
+            if (sp < ego_s && cvs > ego_vs && sp + 50 > ego_s) {
+                const double car_dist = ego_s - sp - P.car_length - P.safety_distance - add;
+                const double sd = cvs - ego_vs;
+                double dtm = sd / P.relaxed_acc;
+                if (T_in == e.ego_lane) dtm += 2;
+                const double md = sd * dtm;
+                if (car_dist < md) open = false;
+            }
+        }
+        open_m &= ~(int)grp_or<G>(valid && !open ? 1u << clane : 0u);
+        // follow cars (src/main.cpp:1391-1409): the in-lane car, the target-lane car of each lane
+        const double s0 = cs + cvs * dt0;
+        const double d0 = cd + cvd * dt0;
+        const int r0 = (int)(threadIdx.x % G), itb = it - r0;    // the group's first iteration index
+        {
+            double k = valid && s0 > ego_s && fabs(d0 - e.ego_d) < 3 ? s0 : kInf;
+            int ki = valid && s0 > ego_s && fabs(d0 - e.ego_d) < 3 ? it : kNone;
+            grp_argmin<G>(k, ki);
+            const int wid = __shfl(id, ki == kNone ? 0 : ki - itb, G);
+            if (ki != kNone && (in_id == -1 || in_s > k || (in_s == k && ki < it_of(2 * NL)))) {
+                in_id = wid; in_s = k; set_it(2 * NL, ki);
+            }
+        }
+#pragma unroll
+        for (int L = 0; L < NL; L++) {
+            const bool q = valid && s0 >= ego_s - P.car_length - P.safety_distance && fabs(d0 - lane_offset(L)) < 3;
+            double k = q ? s0 : kInf;
+            int ki = q ? it : kNone;
+            grp_argmin<G>(k, ki);
+            const int wid = __shfl(id, ki == kNone ? 0 : ki - itb, G);
+            if (ki != kNone && (t_id[L] == -1 || t_s[L] > k || (t_s[L] == k && ki < it_of(NL + L)))) {
+                t_id[L] = wid; t_s[L] = k; set_it(NL + L, ki);
+            }
+        }
+    }
 };
 
-// OR / AND over the G lanes of a group
+
+// TrajectoryBuilder::build start pose (src/main.cpp:583-610): the last kept previous point and the
+// heading of the last kept step, or the ego pose
+__device__ __forceinline__ void start_pose(const pp_scene_batch& in, int64_t S, int64_t s, const EgoSt& e,
+                                           double& pos_x, double& pos_y, double& angle) {
+    if (e.K == 0) {
+        pos_x = e.ego_x; pos_y = e.ego_y;
+        angle = e.yaw * kPi / 180;
+    } else {
+        pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
+        const double vx = pos_x - e.p8x, vy = pos_y - e.p8y;
+        if (vx * vx + vy * vy < kEps) angle = e.yaw * kPi / 180;
+        else angle = ppg::atan2(pos_y - e.p8y, pos_x - e.p8x);       // glibc's atan2, bit for bit
+    }
+}
+// The frame's rotations tv = cos(-a), sin(-a), cos(a), sin(a) as the reference's libm computes
+// them. glibc's sin is odd and its cos even bit for bit (both reduce |x| and apply the sign last;
+// tests/test_glibcm.py checks the restatement on 3.9 M arguments), so two evaluations give all
+// four: cos(-a) = cos(a), sin(-a) = -sin(a). G > 1: lane r of the group computes tv[r] (r < 4;
+// the others hold nothing), except when the restated reduction fails (every lane then holds all
+// four, from the library's own reduction)
 template <int G>
-__device__ __forceinline__ uint32_t grp_or(uint32_t x) {
+__device__ __forceinline__ void frame_trig(double angle, int r, double tv[4]) {
+    bool tfail = false;
+    if (G == 1) {
+        tfail = !ppg::cos(angle, tv[2]);
+        tfail |= !ppg::sin(angle, tv[3]);
+        tv[0] = tv[2];
+        tv[1] = -tv[3];
+    } else {
 #pragma unroll
-    for (int o = G / 2; o >= 1; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o, G);
-    return x;
+        for (int t = 0; t < 4; t++) {
+            if (t % G != r) continue;
+            double v;
+            tfail |= !((t & 1) ? ppg::sin(angle, v) : ppg::cos(angle, v));
+            tv[t] = t == 1 ? -v : v;
+        }
+    }
+    if (G > 1) tfail = grp_or<G>(tfail ? 1u : 0u) != 0u;
+    if (tfail) {                              // every lane: both pairs (rare)
+        double sm, cm, sp, cp;
+        ppm::sincos_pp<true>(-angle, sm, cm);
+        ppm::sincos_pp<true>(angle, sp, cp);
+        tv[0] = cm; tv[1] = sm; tv[2] = cp; tv[3] = sp;
+    }
 }
 
 // The rest of K1 after the car pass (src/main.cpp:447-484, 1358-1438, 583-610, 786-823): scores
@@ -578,15 +724,7 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     }
     // TrajectoryBuilder::build start pose (src/main.cpp:583-610) + frame rotations (:786-823)
     double pos_x, pos_y, angle;
-    if (e.K == 0) {
-        pos_x = e.ego_x; pos_y = e.ego_y;
-        angle = e.yaw * kPi / 180;
-    } else {
-        pos_x = in.prev_x[9 * S + s]; pos_y = in.prev_y[9 * S + s];
-        const double vx = pos_x - e.p8x, vy = pos_y - e.p8y;
-        if (vx * vx + vy * vy < kEps) angle = e.yaw * kPi / 180;
-        else angle = ppg::atan2(pos_y - e.p8y, pos_x - e.p8x);       // glibc's atan2, bit for bit
-    }
+    start_pose(in, S, s, e, pos_x, pos_y, angle);
     // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
     // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
     if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
@@ -604,20 +742,7 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     // them, so the spline and every path position carry their exact bits. Headings of 1e8 rad and
     // more (only from an absurd telemetry yaw) are outside the restated reduction.
     double tv[4];
-    bool tfail = false;
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        if (G > 1 && t % G != r) continue;
-        const double x = t < 2 ? -angle : angle;
-        tfail |= !((t & 1) ? ppg::sin(x, tv[t]) : ppg::cos(x, tv[t]));
-    }
-    if (G > 1) tfail = grp_or<G>(tfail ? 1u : 0u) != 0u;
-    if (tfail) {                              // every lane: both pairs (rare)
-        double sm, cm, sp, cp;
-        ppm::sincos_pp<true>(-angle, sm, cm);
-        ppm::sincos_pp<true>(angle, sp, cp);
-        tv[0] = cm; tv[1] = sm; tv[2] = cp; tv[3] = sp;
-    }
+    frame_trig<G>(angle, r, tv);
     double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
 #pragma unroll
     for (int t = 0; t < 4; t++)
@@ -816,6 +941,11 @@ __device__ __forceinline__ void prep_grp_body(MapG mg, pp_scene_batch in, pp_par
     prep_grp_eval<G>(m, in, P, pv, info, out_status, gb, v, r);
 }
 
+// the grouped K1's planner pass: the group's cars at once (PlanAcc::add_group), or one at a time
+#ifndef PP_GROUP_PASS
+#define PP_GROUP_PASS 1
+#endif
+constexpr bool kGroupPass = PP_GROUP_PASS != 0;
 // One evaluation v by the G lanes of a group (this one is lane r); every lane of the group runs it
 template <int G>
 __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batch& in, const pp_params& P,
@@ -928,13 +1058,17 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
             }
         }
         PP_TRACE_K1(3);
-        const int nq = iters - j0 < G ? iters - j0 : G;
-        for (int q = 0; q < nq; q++) {
-            const int qokl = __shfl(okl, q, G);
-            const int qid = __shfl(id, q, G);
-            const double qcs = __shfl(cs, q, G), qcd = __shfl(cd, q, G);
-            const double qcvs = __shfl(cvs, q, G), qcvd = __shfl(cvd, q, G);
-            if (qokl & 1) a.add(P, e, T_in, j0 + q, qid, qcs, qcd, qokl >> 1, qcvs, qcvd);
+        if (kGroupPass && grp_or<G>((okl & 1) && id == -1 ? 1u : 0u) == 0u) {
+            a.add_group<G>(P, e, T_in, (okl & 1) != 0, j, id, cs, cd, okl >> 1, cvs, cvd);
+        } else {
+            const int nq = iters - j0 < G ? iters - j0 : G;
+            for (int q = 0; q < nq; q++) {
+                const int qokl = __shfl(okl, q, G);
+                const int qid = __shfl(id, q, G);
+                const double qcs = __shfl(cs, q, G), qcd = __shfl(cd, q, G);
+                const double qcvs = __shfl(cvs, q, G), qcvd = __shfl(cvd, q, G);
+                if (qokl & 1) a.add(P, e, T_in, j0 + q, qid, qcs, qcd, qokl >> 1, qcvs, qcvd);
+            }
         }
     }
     PP_TRACE_K1(4);
@@ -1131,16 +1265,18 @@ struct LaneGeom {
     int K, npk, ref_wp;
     double pos_x, pos_y, ca, sa, dist, min_cpd, ratio, ego_d;
 };
-__device__ __forceinline__ LaneGeom lane_geom(const PrepV& pv, int64_t v, int64_t Sv, int L) {
+// (from the K1 values it reads: the build's start pose and rotation, the ego's Frenet state)
+__device__ __forceinline__ LaneGeom lane_geom_from(int K, double pos_x, double pos_y, double ca_m, double sa_m,
+                                                   int ref_wp, double ratio_L, double ego_d, double start,
+                                                   double ego_vd, int L) {
     LaneGeom g;
-    g.K = pv.K[v];
+    g.K = K;
     g.npk = g.K > 0 ? g.K - 1 : 0;
-    g.pos_x = pv.pos_x[v]; g.pos_y = pv.pos_y[v];
-    g.ca = pv.ca_m[v]; g.sa = pv.sa_m[v];
-    g.ref_wp = pv.ref_wp[v];
-    g.ratio = pv.ratio[L * Sv + v];
-    g.ego_d = pv.ego_d[v];
-    const double start = pv.ego_speed[v], ego_vd = pv.ego_vd[v];
+    g.pos_x = pos_x; g.pos_y = pos_y;
+    g.ca = ca_m; g.sa = sa_m;
+    g.ref_wp = ref_wp;
+    g.ratio = ratio_L;
+    g.ego_d = ego_d;
     double min_cpd = start * 1;
     g.min_cpd = s_max(min_cpd, 5.0);
     const double d_diff = lane_offset(L) - g.ego_d;
@@ -1163,6 +1299,10 @@ __device__ __forceinline__ LaneGeom lane_geom(const PrepV& pv, int64_t v, int64_
     if (dist > 50) dist = 50;
     g.dist = dist;
     return g;
+}
+__device__ __forceinline__ LaneGeom lane_geom(const PrepV& pv, int64_t v, int64_t Sv, int L) {
+    return lane_geom_from(pv.K[v], pv.pos_x[v], pv.pos_y[v], pv.ca_m[v], pv.sa_m[v], pv.ref_wp[v],
+                          pv.ratio[L * Sv + v], pv.ego_d[v], pv.ego_speed[v], pv.ego_vd[v], L);
 }
 
 __device__ void team_a1(const MapV& m, const pp_scene_batch& in, const LaneGeom& g, int64_t s, int L,
@@ -1630,11 +1770,18 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 // One group g of the candidate grid (BPS == 1: scenes [g SPB, g SPB + SPB); BPS > 1: candidates
 // [coff, coff + 256) of scene g / BPS) by the whole workgroup. Every barrier inside is reached by
 // all threads of the block (the early return is block-uniform).
-template <bool kSlow, int kMode, bool kEmitIn = false>
+// kEmitIn (reference mode, kMode 1): 0 the winners' paths are replayed by k_emit; 1 by the block
+// after phase B (K4 in the block, below); 2 the winner lanes write their points during the loop
+// (output mode 2: the transform and its turns in the step, no record and no replay — the
+// single-frame and small-batch step, whose time is the winners' serial chain)
+// kPreA: the block's (single) scene has its fast-path spline slots built already (k_plan_frame's
+// second wave builds them while the first runs K1): phase A is skipped
+template <bool kSlow, int kMode, int kEmitIn = 0, bool kPreA = false>
 __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
                                            const PrepV& pv, const pp_result& out, int SPB, int BPS,
                                            double* rec, uint64_t* adjm, int64_t g, double* sm) {
-    constexpr bool emit_in = kEmitIn && kMode == 1;
+    constexpr bool emit_in = kEmitIn == 1 && kMode == 1;
+    constexpr bool win_inline = kEmitIn == 2 && kMode == 1;
     const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
     const int D = P.n_draws > 1 ? P.n_draws : 1;
     const int C = D * Cv;                     // candidates per scene (all draws)
@@ -1671,8 +1818,10 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     }
 #endif
 #ifdef PP_CHECK
-    for (int i = tid; i < 5 * nslot * kKP; i += (int)blockDim.x) sX[i] = __builtin_nan("");
-    for (int i = tid; i < 4 * nslot; i += (int)blockDim.x) sMeta[i] = kMetaPoison;
+    if (!kPreA) {
+        for (int i = tid; i < 5 * nslot * kKP; i += (int)blockDim.x) sX[i] = __builtin_nan("");
+        for (int i = tid; i < 4 * nslot; i += (int)blockDim.x) sMeta[i] = kMetaPoison;
+    }
 #endif
     __syncthreads();
     bool mine = false;
@@ -1681,7 +1830,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         if (pv.lim_mask[(s0 + q) * D + (t - q * D)] & kLimSlow) { atomicOr(&sSlow[q], 1u); mine = true; }
     }
     if (!__syncthreads_or(mine) && kSlow) return;      // whole block leaves: no flagged scene
-    {   // phase A: a team of TS threads per slot (team_a1..a5), block barriers between the steps
+    if (!kPreA) {   // phase A: a team of TS threads per slot (team_a1..a5), block barriers between the steps
         int TS = (int)blockDim.x / nslot;
         if (TS > 8) TS = 8;
         const int j = tid / TS, r = tid - j * TS;
@@ -1786,6 +1935,30 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 st_xy(px + i * ps, __builtin_nan(""), __builtin_nan(""));
             }
             if (out.path_len && PP_CHK(s * C + c < g_lim.ncost, 11, s * C + c)) out.path_len[s * C + c] = K + R.ng;
+            if (winner) {
+                for (int i = K + R.ng; i < N; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 10)) break;
+                    out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0;
+                }
+                out.n_out[s] = K + R.ng;
+                out.winner[s] = c;
+            }
+        } else if (win_inline && tid < 64) {
+            // reference mode, the block's first wave: the winners write next_x/next_y in the loop
+            // (the rest of the wave runs the same instantiation without outputs, in lockstep)
+            double* wx = nullptr;
+            double* wy = nullptr;
+            if (winner) {
+                for (int i = 0; i < K; i++) {
+                    if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 9)) break;
+                    out.next_x[(int64_t)i * S + s] = in.prev_x[(int64_t)i * S + s];
+                    out.next_y[(int64_t)i * S + s] = in.prev_y[(int64_t)i * S + s];
+                }
+                wx = out.next_x + (int64_t)K * S + s;
+                wy = out.next_y + (int64_t)K * S + s;
+            }
+            R = run_candidate<kSlow, 2>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v], pv.ca_p[v], pv.sa_p[v],
+                                        sc, N - K, wx, wy, S, nullptr, 0);
             if (winner) {
                 for (int i = K + R.ng; i < N; i++) {
                     if (!PP_CHKP(out.next_x + (int64_t)i * S + s, nx, nnext, 10)) break;
@@ -2164,10 +2337,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         uint64_t* adjm, uint32_t* gbits) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int64_t g = blockIdx.x;
-    cand_group<false, 1, true>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+    cand_group<false, 1, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
     __syncthreads();
     if ((gbits[g >> 5] >> (g & 31)) & 1u) {                   // same word for every lane
-        cand_group<true, 1, true>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
+        cand_group<true, 1, 1>(mg, in, P, pv, out, SPB, 1, rec, adjm, g, sm);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
@@ -2179,14 +2352,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // phase A reading the same LDS map. The prep record goes through global memory inside the block
 // (written, barrier, read by the same workgroup). No kernel boundary is left in the step.
 // ------------------------------------------------------------------------------------------------
+#ifndef PP_STEP_EMIT
+#define PP_STEP_EMIT 2
+#endif
+// the winners' output in the one-launch step (cand_group kEmitIn): inline (2) or replayed (1)
+constexpr int kStepEmit = PP_STEP_EMIT;
 __device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
                                                 const PrepV& pv, const pp_result& out, int SPB, double* rec,
                                                 uint64_t* adjm) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int n = mg.n;
 #ifdef PP_TRACE
-    // (block 0: start, after K1, after the fast scenes' K2 + K4, end; words at group kTraceK1 - 1)
-    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 0);
+    // (block 0: start, after K1, after the fast scenes' K2 + K4, end; words at group kTraceK1 - 1;
+    // the shader clock (s_memtime) beside the constant clock at start and end, group kTraceK1 - 3)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        trace_at(kTraceK1 - 1, 0);
+        g_trace[8 * (kTraceK1 - 3) + 0] = wall_clock64();
+        g_trace[8 * (kTraceK1 - 3) + 1] = clock64();
+    }
 #endif
     stage_map(sm, mg.buf, kMapArrays * n);
     __syncthreads();
@@ -2204,16 +2387,112 @@ __device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& i
 #endif
     const MapG ml = {sm, n, mg.fastm};
     double* csm = sm + ((kMapArrays * n + 1) & ~1);
-    cand_group<false, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
+    cand_group<false, 1, kStepEmit>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
     __syncthreads();
 #ifdef PP_TRACE
     if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 2);
 #endif
-    cand_group<true, 1, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
+    cand_group<true, 1, kStepEmit>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
 #ifdef PP_TRACE
-    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 3);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        trace_at(kTraceK1 - 1, 3);
+        g_trace[8 * (kTraceK1 - 3) + 2] = wall_clock64();
+        g_trace[8 * (kTraceK1 - 3) + 3] = clock64();
+    }
 #endif
 }
+// One frame (SPB slots, scene 0 only) with two waves at work before phase B: the first runs K1 (16
+// lanes), the second derives the ego state and the build's start pose itself (the same operations
+// on the same inputs: the same bits as K1's record) and builds the scene's NL spline slots (phase A
+// needs neither the cars nor the planner), so phase A leaves the frame's critical path. The
+// team's steps synchronise by wave (one instruction stream; LDS is in order within a wave).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void frame_phase_a(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                              int SPB, double* sm, int l) {
+    const int64_t S = in.n_scenes, s = 0;
+    EgoSt e;
+    prep_ego<16>(m, in, P, S, s, l % 16, e);      // (four identical groups of 16 lanes)
+    double pos_x, pos_y, angle;
+    start_pose(in, S, s, e, pos_x, pos_y, angle);
+    double tv[4];
+    frame_trig<16>(angle, l % 16, tv);
+    const double ca_m = __shfl(tv[0], 0, 16), sa_m = __shfl(tv[1], 1, 16);
+    const int nslot = NL * SPB;
+    double* sX = sm;
+    int* sMeta = (int*)(sX + 5 * nslot * kKP);
+    int TS = 64 / NL;
+    if (TS > 8) TS = 8;
+    const int j = l / TS, r = l - j * TS;
+    const bool act = j < NL;
+    const int L = act ? j : 0;
+    const Slot sl = lds_slot(sX, nslot, sMeta, L);
+    double ratio_L = e.ratio[0];
+#pragma unroll
+    for (int k = 1; k < NL; k++) if (L == k) ratio_L = e.ratio[k];
+    const LaneGeom g = lane_geom_from(e.K, pos_x, pos_y, ca_m, sa_m, e.ref_wp, ratio_L, e.ego_d,
+                                      e.ego_speed, e.ego_vd, L);
+    if (act) team_a1(m, in, g, s, L, sl, r, TS);
+    wave_sync();
+    const bool act_s = l < NL;                    // the serial steps: one lane per slot
+    const Slot sls = lds_slot(sX, nslot, sMeta, act_s ? l : 0);
+    if (act_s) team_a2(g, sls);
+    wave_sync();
+    if (act) team_a3(sl, r, TS);
+    wave_sync();
+    if (act_s) team_a4(sls);
+    wave_sync();
+    if (act) team_a5(sl, r, TS);
+}
+
+__device__ __forceinline__ void frame_step_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
+                                                const PrepV& pv, const pp_result& out, int SPB, double* rec,
+                                                uint64_t* adjm) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int n = mg.n;
+#ifdef PP_TRACE
+    if (threadIdx.x == 0) {
+        trace_at(kTraceK1 - 1, 0);
+        g_trace[8 * (kTraceK1 - 3) + 0] = wall_clock64();
+        g_trace[8 * (kTraceK1 - 3) + 1] = clock64();
+    }
+#endif
+    stage_map(sm, mg.buf, kMapArrays * n);
+    __syncthreads();
+    const MapV m = map_view(sm, n, mg.fastm);
+    double* csm = sm + ((kMapArrays * n + 1) & ~1);
+    if (threadIdx.x < 16) {                       // K1 of scene 0 (16 lanes of the first wave)
+        const GroupBits nobits = {nullptr, SPB, 1, nullptr, nullptr};
+        prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, 0, (int)threadIdx.x);
+    } else if (threadIdx.x >= 64 && threadIdx.x < 128) {
+        frame_phase_a(m, in, P, SPB, csm, (int)threadIdx.x - 64);
+#ifdef PP_TRACE
+        if (threadIdx.x == 64) trace_at(kTraceK1 - 4, 0);
+#endif
+    }
+    __syncthreads();
+#ifdef PP_TRACE
+    if (threadIdx.x == 0) trace_at(kTraceK1 - 1, 1);
+#endif
+    const MapG ml = {sm, n, mg.fastm};
+    cand_group<false, 1, kStepEmit, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, 0, csm);
+    __syncthreads();
+#ifdef PP_TRACE
+    if (threadIdx.x == 0) trace_at(kTraceK1 - 1, 2);
+#endif
+    cand_group<true, 1, kStepEmit>(ml, in, P, pv, out, SPB, 1, rec, adjm, 0, csm);
+#ifdef PP_TRACE
+    if (threadIdx.x == 0) {
+        trace_at(kTraceK1 - 1, 3);
+        g_trace[8 * (kTraceK1 - 3) + 2] = wall_clock64();
+        g_trace[8 * (kTraceK1 - 3) + 3] = clock64();
+    }
+#endif
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small(
         MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
         uint64_t* adjm) {
@@ -2227,6 +2506,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // frame is done — no copy commands and no stream synchronisation per frame.
 // Ranges are 4-byte-word ranges of the frame (host and device share the layout).
 // ------------------------------------------------------------------------------------------------
+#ifndef PP_FRAME_WAVES
+#define PP_FRAME_WAVES 1      // phase A on the block's second wave, beside K1 (frame_step_body)
+#endif
 constexpr int kFioMax = 16;
 struct FrameIO {
     const uint32_t* h_in;     // pinned host frame (inputs)
@@ -2268,7 +2550,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     frame_copy<8>(io.h_in, io.d_frame, io.n_in, io.in_off, io.in_len);
     __threadfence_block();
     __syncthreads();
+#if PP_FRAME_WAVES
+    frame_step_body(mg, in, P, pv, out, SPB, rec, adjm);
+#else
     step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+#endif
     __threadfence_block();
     __syncthreads();
     frame_copy<8>(io.d_frame, io.h_out, io.n_out, io.out_off, io.out_len);
@@ -3668,7 +3954,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     }
     Frame& h = *(Frame*)DS.frame_host;
     volatile uint32_t* flag = (volatile uint32_t*)((char*)DS.frame_host + kFlagOff);
-    memset(&h, 0, sizeof(h));
+    // (only the words the frame's ranges carry are written: the previous path's unused tail is
+    // zeroed, every other input range is filled below)
+    memset(h.px, 0, sizeof h.px); memset(h.py, 0, sizeof h.py);
     const bool poison = dbg(PP_DBG_POISON) != 0;
     if (poison) {     // the outputs' staging starts NaN-filled (pp_eval poisons them on the device too)
         memset(h.nx, 0xFF, sizeof h.nx); memset(h.ny, 0xFF, sizeof h.ny); memset(h.cost, 0xFF, sizeof h.cost);
@@ -3683,8 +3971,10 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     }
     // the reference's std::map, laid out over the union of its ids and this frame's (any ints)
     const pptab::Slots hs = {1, h.tid, h.tvalid, h.tlane, h.ts, h.td, h.tvs, h.tvd, h.tvx, h.tvy};
-    const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, TS, poison);
-    if (nslots < 0) return PP_ERR_ARG;                  // more than PP_MAX_CARS distinct cars
+    const int nu = DS.plan_table.union_size(h.cid, nc);
+    if (nu > TS) return PP_ERR_ARG;                     // more than PP_MAX_CARS distinct cars
+    const int nslots = DS.plan_table.layout(h.cid, nc, hs, 0, nu, poison);
+    if (nslots < 0) return PP_ERR_ARG;
     hipStream_t st = DS.frame_stream;
     pp_scene_batch B;
     memset(&B, 0, sizeof(B));

@@ -81,3 +81,17 @@ def test_device_build_equals_glibc():
         assert same(got, oracle_lib.glibc_batch(olib, k, x)), k
     got = ppamd.libm_eval("atan2", torch.from_numpy(y).to(dev), torch.from_numpy(z).to(dev), device=0).cpu().numpy()
     assert same(got, oracle_lib.glibc_batch(olib, "atan2", y, z))
+
+
+def test_sin_odd_cos_even_bitwise():
+    """k_prep's frame rotations take cos(-a) = cos(a) and sin(-a) = -sin(a) (two evaluations for
+    four): both glibc and the restatement reduce |x| and apply the sign last, so the identities
+    hold bit for bit (NaN aside) over headings, small, medium and large arguments."""
+    olib = oracle_lib.load_oracle()
+    x, _, _ = args(300_000, 3)
+    x = x[np.isfinite(x)]
+    for lib in ("restated", "glibc"):
+        ev = (lambda k, a: ppamd.libm_eval(k, a)) if lib == "restated" else \
+             (lambda k, a: oracle_lib.glibc_batch(olib, k, a))
+        assert same(ev("cos", -x), ev("cos", x)), lib
+        assert same(ev("sin", -x), -ev("sin", x)), lib

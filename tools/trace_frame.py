@@ -40,13 +40,15 @@ def main():
         k = t[K1_BASE - 1]            # k_step_small: start, after K1, after K2 + K4, end
         q = t[K1_BASE - 2]            # K1 of the scene (lane 0): start, ego, row search, walks, pass, finish
         g = t[0]                      # cand_group: start, phase A end, phase B end per wave, end, K4 table
+        c = t[K1_BASE - 3]            # constant clock and shader clock at start and end
         res.append({"map_stage_us": (q[0] - k[0]) / 100, "k1_ego_us": (q[1] - q[0]) / 100,
                     "k1_row_search_us": (q[2] - q[1]) / 100, "k1_car_walks_us": (q[3] - q[2]) / 100,
                     "k1_planner_pass_us": (q[4] - q[3]) / 100, "k1_finish_us": (q[5] - q[4]) / 100,
                     "k1_us": (k[1] - k[0]) / 100, "k2_entry_us": (g[0] - k[1]) / 100,
                     "phase_a_us": (g[1] - g[0]) / 100, "phase_b_us": (g[2:6].max() - g[1]) / 100,
                     "k4_table_us": (g[7] - g[6]) / 100, "k4_replay_us": (k[2] - g[7]) / 100,
-                    "slow_pass_us": (k[3] - k[2]) / 100, "total_us": (k[3] - k[0]) / 100})
+                    "slow_pass_us": (k[3] - k[2]) / 100, "total_us": (k[3] - k[0]) / 100,
+                    "wave1_phase_a_done_us": (t[K1_BASE - 4][0] - k[0]) / 100})
     out = {k: float(np.median([r[k] for r in res])) for k in res[0]}
     print(json.dumps({"what": "k_step_small phases of pp_plan_frame (median of 50 frames, 100 MHz clock)", **out}))
 
