@@ -602,7 +602,7 @@ def main(argv=None):
     # the same fraction from the profiler's average K2 duration of this exact launch shape (a
     # committed rocprofv3 run of this command; durations do not carry over between batch sizes)
     rp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D))
-    rp = rp if rp and rp.get("launches_per_step") == k2_per_step else None
+    rp = rp if rp and rp.get("launches_per_step") == k2_per_step and not a.rollout else None
     wname = workload_name(S, Cn, a.n_speeds, a.n_points, a.emit_paths, D, a.rollout)
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",

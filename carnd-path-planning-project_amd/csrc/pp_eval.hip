@@ -3595,7 +3595,20 @@ int32_t pp_debug_get(int32_t key) { return key >= 0 && key < PP_DBG_KEYS ? dbg(k
 int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
     if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
     std::lock_guard<std::mutex> lk(M->mu);
-    M->dev[device].timing = enable != 0;
+    DevState& D = M->dev[device];
+    D.timing = enable != 0;
+    if (D.timing) {
+        // the events of 256 calls made now, outside any timed region (pp_eval takes 8 per call
+        // from the pool, pp_timing_read returns them)
+        DeviceGuard g(device);
+        const int rc = dev_init(M, device);       // (pp_map_destroy frees the events of initialised devices)
+        if (rc) return rc;
+        while (D.ev_pool.size() + D.ev_rec.size() < 8 * 256) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
+            D.ev_pool.push_back(e);
+        }
+    }
     return PP_OK;
 }
 
