@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cmath>
 #include <map>
@@ -2504,30 +2505,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // device frame by the block itself, k_step_small's body runs, the output ranges are written back
 // to pinned host memory, and a sequence number in host memory tells the waiting host thread the
 // frame is done — no copy commands and no stream synchronisation per frame.
-// Ranges are 4-byte-word ranges of the frame (host and device share the layout).
+// Ranges are 16-byte-unit ranges of the frame (host and device share the layout; the host rounds
+// each field's range out to whole units and merges neighbours): one 16-B load per unit, since
+// the reads cross PCIe as one transaction per load.
 // ------------------------------------------------------------------------------------------------
 #ifndef PP_FRAME_WAVES
 #define PP_FRAME_WAVES 1      // phase A on the block's second wave, beside K1 (frame_step_body)
 #endif
 constexpr int kFioMax = 16;
+constexpr int kFioInline = 176;   // 16-B units of input carried in the kernel arguments (2.75 KB)
 struct FrameIO {
-    const uint32_t* h_in;     // pinned host frame (inputs)
-    uint32_t* d_frame;        // device frame
-    uint32_t* h_out;          // pinned host frame (outputs)
+    const uint4* h_in;        // pinned host frame (inputs)
+    uint4* d_frame;           // device frame
+    uint4* h_out;             // pinned host frame (outputs)
     uint32_t* h_flag;         // pinned host word: seq once the outputs are in place
     uint32_t seq;
     int n_in, n_out;
-    uint32_t in_off[kFioMax], in_len[kFioMax], out_off[kFioMax], out_len[kFioMax];   // words
+    uint32_t in_off[kFioMax], in_len[kFioMax], out_off[kFioMax], out_len[kFioMax];   // 16-B units
+    // inputs of up to kFioInline units (a frame of up to ~25 cars) ride in the kernel arguments,
+    // which the launch writes to device memory: the block reads them there instead of across
+    // PCIe (n_inl: the units held, in range order; 0: read the ranges from h_in)
+    int n_inl;
+    uint4 inl[kFioInline];
 };
-// words [0, total) of the ranges, thread t taking t, t + blockDim.x, ...: every thread's loads are
-// issued before its stores (one round trip to the host per kChunk words)
+// units [0, total) of the ranges, thread t taking t, t + blockDim.x, ...: every thread's loads are
+// issued before its stores (one round trip to the host per kChunk units)
 template <int kChunk>
-__device__ __forceinline__ void frame_copy(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+__device__ __forceinline__ void frame_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                            int nr, const uint32_t* off, const uint32_t* len) {
     uint32_t total = 0;
     for (int r = 0; r < nr; r++) total += len[r];
     for (uint32_t w0 = threadIdx.x; w0 < total; w0 += kChunk * blockDim.x) {
-        uint32_t v[kChunk], at[kChunk];
+        uint4 v[kChunk];
+        uint32_t at[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
             uint32_t w = w0 + u * blockDim.x;
@@ -2536,7 +2546,7 @@ __device__ __forceinline__ void frame_copy(const uint32_t* __restrict__ src, uin
                 int r = 0;
                 while (w >= len[r]) { w -= len[r]; r++; }
                 at[u] = off[r] + w;
-                v[u] = __builtin_nontemporal_load(src + at[u]);
+                v[u] = src[at[u]];
             }
         }
 #pragma unroll
@@ -2544,12 +2554,31 @@ __device__ __forceinline__ void frame_copy(const uint32_t* __restrict__ src, uin
             if (at[u] != 0xffffffffu) dst[at[u]] = v[u];
     }
 }
+// (io is the first kernel argument: offset 0 of the kernel-argument segment)
+constexpr size_t kFioArgOff = 0;
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_plan_frame(
-        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
-        uint64_t* adjm, FrameIO io) {
-    frame_copy<8>(io.h_in, io.d_frame, io.n_in, io.in_off, io.in_len);
+        FrameIO io, MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm) {
+#ifdef PP_FRAME_PROF
+    const uint64_t t_in = wall_clock64();
+#endif
+    if (io.n_inl > 0) {
+        // the kernel-argument copy: units in range order (thread t: units t, t + blockDim.x)
+        const uint4* src = (const uint4*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + kFioArgOff +
+                                          offsetof(FrameIO, inl));
+        for (int w0 = (int)threadIdx.x; w0 < io.n_inl; w0 += (int)blockDim.x) {
+            int w = w0, r = 0;
+            while (w >= (int)io.in_len[r]) { w -= (int)io.in_len[r]; r++; }
+            io.d_frame[io.in_off[r] + w] = src[w0];
+        }
+    } else {
+        frame_copy<4>(io.h_in, io.d_frame, io.n_in, io.in_off, io.in_len);
+    }
     __threadfence_block();
     __syncthreads();
+#ifdef PP_FRAME_PROF
+    const uint64_t t_body = wall_clock64();
+#endif
 #if PP_FRAME_WAVES
     frame_step_body(mg, in, P, pv, out, SPB, rec, adjm);
 #else
@@ -2557,7 +2586,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #endif
     __threadfence_block();
     __syncthreads();
-    frame_copy<8>(io.d_frame, io.h_out, io.n_out, io.out_off, io.out_len);
+#ifdef PP_FRAME_PROF
+    const uint64_t t_out = wall_clock64();
+#endif
+    frame_copy<4>(io.d_frame, io.h_out, io.n_out, io.out_off, io.out_len);
+#ifdef PP_FRAME_PROF
+    if (threadIdx.x == 0) { io.h_flag[4] = (uint32_t)t_in; io.h_flag[5] = (uint32_t)t_body; io.h_flag[6] = (uint32_t)t_out; io.h_flag[7] = (uint32_t)wall_clock64(); }
+#endif
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(io.h_flag, io.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3431,8 +3466,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
         const int threads_f = std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
         if (fio) {
-            hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, mg, B, P, pv, R, spb_f, rec,
-                               adjm, *fio);
+            hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, *fio, mg, B, P, pv, R, spb_f,
+                               rec, adjm);
         } else {
             hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
                                R, spb_f, rec, adjm);
@@ -3911,6 +3946,20 @@ int32_t pp_plan_reset(pp_map* M, int32_t device) {
 }
 
 // One telemetry frame (the onMessage replacement): C = 3 (one speed: max_speed), reference mode.
+#ifdef PP_FRAME_PROF
+// diagnostic builds (-DPP_FRAME_PROF): per-frame host and device intervals, summed (us) — host:
+// staging until the launch, the launch call, launch-to-done, done-to-return; device (100 MHz
+// clock): input copy, the frame's body, output copy; and the frame count. pp_frame_prof_read
+// returns and clears them.
+static double g_fprof[8];
+static double fprof_now() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+int32_t pp_frame_prof_read(double* out8) {
+    for (int i = 0; i < 8; i++) { out8[i] = g_fprof[i]; g_fprof[i] = 0; }
+    return PP_OK;
+}
+#endif
 int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, double ego_yaw_deg,
                       double ego_speed_mph, const double* prev_x, const double* prev_y, int32_t n_prev,
                       const int32_t* car_id, const double* car_x, const double* car_y,
@@ -3921,6 +3970,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         (n_cars > 0 && (!car_id || !car_x || !car_y || !car_vx || !car_vy)))
         return PP_ERR_ARG;
     if (*target_lane < 0 || *target_lane >= NL) return PP_ERR_ARG;
+#ifdef PP_FRAME_PROF
+    const double h0 = fprof_now();
+#endif
     // host staging: one scene, SoA with S = 1 (std::map order: stable sort by id, last row of a
     // duplicated id wins as in `sensor_fusion_cars[id]` assignment, src/main.cpp:1329)
     struct Row { int32_t id; double x, y, vx, vy; };
@@ -3954,7 +4006,8 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
         std::lock_guard<std::mutex> lk(M->mu);
         int rc = dev_init(M, device);
         if (rc) return rc;
-        if (!DS.frame && hipMalloc(&DS.frame, sizeof(Frame)) != hipSuccess) return PP_ERR_NOMEM;
+        // (both copies kFlagOff bytes: the 16-B units of the last fields may pass sizeof(Frame))
+        if (!DS.frame && hipMalloc(&DS.frame, kFlagOff) != hipSuccess) return PP_ERR_NOMEM;
         if (!DS.frame_host) {
             if (hipHostMalloc(&DS.frame_host, kFlagOff + 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
                 return PP_ERR_NOMEM;
@@ -4008,13 +4061,22 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     // The frame's words that carry data: inputs (ego, previous path, this frame's rows, the table's
     // nslots slots) and outputs (plan, costs, winner / count / status / info, the slots again).
     FrameIO io;
-    memset(&io, 0, sizeof(io));
+    memset(&io, 0, offsetof(FrameIO, inl));
+    // (each field's bytes rounded out to whole 16-B units: the extra words are other fields of the
+    // frame — inputs the kernel overwrites nothing of, outputs the host does not read — and a unit
+    // range touching the previous one joins it)
     auto add = [&](bool in, const void* p, size_t bytes) {
-        const uint32_t off = (uint32_t)(((const char*)p - (const char*)&h) / 4), len = (uint32_t)(bytes / 4);
-        if (!len) return;
+        if (!bytes) return;
+        const size_t b0 = (size_t)((const char*)p - (const char*)&h);
+        const uint32_t u0 = (uint32_t)(b0 / 16), u1 = (uint32_t)((b0 + bytes + 15) / 16);
         int& n = in ? io.n_in : io.n_out;
-        (in ? io.in_off : io.out_off)[n] = off;
-        (in ? io.in_len : io.out_len)[n] = len;
+        uint32_t* off = in ? io.in_off : io.out_off;
+        uint32_t* len = in ? io.in_len : io.out_len;
+        if (n > 0 && u0 <= off[n - 1] + len[n - 1] && u0 >= off[n - 1]) {
+            if (u1 > off[n - 1] + len[n - 1]) len[n - 1] = u1 - off[n - 1];
+            return;
+        }
+        off[n] = u0; len[n] = u1 - u0;
         n++;
     };
     const size_t ns = (size_t)nslots, ncs = (size_t)nc;
@@ -4035,12 +4097,28 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
                   offsetof(Frame, cost) == offsetof(Frame, ny) + sizeof(double) * N &&
                   offsetof(Frame, cid) == offsetof(Frame, nprev) + 12 && sizeof(pp_scene_info) % 4 == 0,
                   "adjacent frame fields");
+    {   // the input units in range order, inline where they fit
+        int nu = 0;
+        for (int r = 0; r < io.n_in; r++) nu += (int)io.in_len[r];
+        io.n_inl = 0;
+        if (nu <= kFioInline) {
+            const uint4* hu = (const uint4*)&h;
+            for (int r = 0; r < io.n_in; r++)
+                for (uint32_t w = 0; w < io.in_len[r]; w++) io.inl[io.n_inl++] = hu[io.in_off[r] + w];
+        }
+    }
     void* hdev = nullptr;
     if (hipHostGetDevicePointer(&hdev, DS.frame_host, 0) != hipSuccess) return PP_ERR_HIP;
-    io.h_in = (const uint32_t*)hdev; io.h_out = (uint32_t*)hdev; io.d_frame = (uint32_t*)d;
+    io.h_in = (const uint4*)hdev; io.h_out = (uint4*)hdev; io.d_frame = (uint4*)d;
     io.h_flag = (uint32_t*)((char*)hdev + kFlagOff);
     io.seq = ++DS.frame_seq;
+#ifdef PP_FRAME_PROF
+    const double h1 = fprof_now();
+#endif
     int rc = eval_impl(M, &B, &P, &R, device, (void*)st, &io);
+#ifdef PP_FRAME_PROF
+    const double h2 = fprof_now();
+#endif
     if (rc == PP_OK) {
         // the kernel's done word; the stream is polled now and then, so a failed launch or a fault
         // ends the wait with an error
@@ -4053,6 +4131,14 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
             __builtin_ia32_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+#ifdef PP_FRAME_PROF
+        const double h3 = fprof_now();
+        const volatile uint32_t* fw = flag;
+        g_fprof[0] += h1 - h0; g_fprof[1] += h2 - h1; g_fprof[2] += h3 - h2;
+        g_fprof[4] += (uint32_t)(fw[5] - fw[4]) / 100.0; g_fprof[5] += (uint32_t)(fw[6] - fw[5]) / 100.0;
+        g_fprof[6] += (uint32_t)(fw[7] - fw[6]) / 100.0; g_fprof[7] += 1;
+        g_fprof[3] -= h3;             // (done-to-return: the return adds its time)
+#endif
     } else if (rc == PP_ERR_STATE) {
         // a launch shape other than the one-launch step (debug shapes, maps beyond the LDS): copies
         if (hipMemcpyAsync(d, &h, sizeof(Frame), hipMemcpyHostToDevice, st) != hipSuccess) return PP_ERR_HIP;
@@ -4066,6 +4152,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     *n_out = h.nout;
     for (int i = 0; i < h.nout && i < N; i++) { next_x[i] = h.nx[i]; next_y[i] = h.ny[i]; }
     *target_lane = h.info.target_lane;
+#ifdef PP_FRAME_PROF
+    g_fprof[3] += fprof_now();
+#endif
     return PP_OK;
 }
 
