@@ -2358,6 +2358,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #endif
 // the winners' output in the one-launch step (cand_group kEmitIn): inline (2) or replayed (1)
 constexpr int kStepEmit = PP_STEP_EMIT;
+// the one-launch step with phase A beside K1 (wave_step_body) where the blocks allow it
+#ifndef PP_STEP_WAVES
+#define PP_STEP_WAVES 1
+#endif
+constexpr bool kStepWaves = PP_STEP_WAVES != 0;
+// doubles of k_cand's LDS for SPB scenes (cand_geom_lds, host), rounded up
+__host__ __device__ constexpr int cand_lds_doubles(int spb) {
+    return (int)(((sizeof(double) * 5 * kKP * (NL * spb) + sizeof(int) * 4 * (NL * spb) + sizeof(uint32_t) * 2 * spb + 7) / 8 * 8 +
+                  sizeof(uint64_t) * 2 * spb + sizeof(int) * spb + 7) / 8);
+}
 __device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
                                                 const PrepV& pv, const pp_result& out, int SPB, double* rec,
                                                 uint64_t* adjm) {
@@ -2402,102 +2412,141 @@ __device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& i
     }
 #endif
 }
-// One frame (SPB slots, scene 0 only) with two waves at work before phase B: the first runs K1 (16
-// lanes), the second derives the ego state and the build's start pose itself (the same operations
-// on the same inputs: the same bits as K1's record) and builds the scene's NL spline slots (phase A
-// needs neither the cars nor the planner), so phase A leaves the frame's critical path. The
-// team's steps synchronise by wave (one instruction stream; LDS is in order within a wave).
+// The one-launch step with phase A off the critical path (k_plan_frame, and k_step_small for blocks
+// of up to kStepWaveSpb scenes): waves 0-1 run K1 (16 lanes per scene) while waves 2-3 derive each
+// scene's ego state and the build's start pose themselves (K1's own functions on the same inputs:
+// the same bits as K1's record) and build the scenes' NL spline slots — phase A needs neither the
+// cars nor the planner. Wave 2 takes scenes 0-3, wave 3 scenes 4-7; each wave's steps synchronise
+// by wave (one instruction stream; LDS is in order within a wave), the per-scene geometry passing
+// through an LDS record of kGeoD doubles per scene.
+constexpr int kStepWaveSpb = 8;
+constexpr int kGeoD = 16;
+static_assert(10 + NL <= kGeoD, "geometry record");
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ void frame_phase_a(const MapV& m, const pp_scene_batch& in, const pp_params& P,
-                                              int SPB, double* sm, int l) {
-    const int64_t S = in.n_scenes, s = 0;
-    EgoSt e;
-    prep_ego<16>(m, in, P, S, s, l % 16, e);      // (four identical groups of 16 lanes)
-    double pos_x, pos_y, angle;
-    start_pose(in, S, s, e, pos_x, pos_y, angle);
-    double tv[4];
-    frame_trig<16>(angle, l % 16, tv);
-    const double ca_m = __shfl(tv[0], 0, 16), sa_m = __shfl(tv[1], 1, 16);
+// wave w of the phase-A waves, lane l: scenes [4 w, 4 w + 4) of the block's nsc
+__device__ __forceinline__ void wave_phase_a(const MapV& m, const pp_scene_batch& in, const pp_params& P,
+                                             int SPB, double* sm, double* geo, int64_t s0, int nsc, int w, int l) {
+    const int64_t S = in.n_scenes;
+    {   // the ego state, start pose and rotations of scene q by 16 lanes; lane 0 records them
+        const int q = 4 * w + l / 16, r = l % 16;
+        if (q < nsc) {                                // (group-uniform)
+            const int64_t s = s0 + q;
+            EgoSt e;
+            prep_ego<16>(m, in, P, S, s, r, e);
+            double pos_x, pos_y, angle;
+            start_pose(in, S, s, e, pos_x, pos_y, angle);
+            double tv[4];
+            frame_trig<16>(angle, r, tv);
+            const double ca_m = __shfl(tv[0], 0, 16), sa_m = __shfl(tv[1], 1, 16);
+            if (r == 0) {
+                double* gq = geo + q * kGeoD;
+                gq[0] = e.K; gq[1] = pos_x; gq[2] = pos_y; gq[3] = ca_m; gq[4] = sa_m; gq[5] = e.ref_wp;
+                gq[6] = e.ego_d; gq[7] = e.ego_speed; gq[8] = e.ego_vd;
+#pragma unroll
+                for (int k = 0; k < NL; k++) gq[9 + k] = e.ratio[k];
+            }
+        }
+    }
+    wave_sync();
     const int nslot = NL * SPB;
     double* sX = sm;
     int* sMeta = (int*)(sX + 5 * nslot * kKP);
-    int TS = 64 / NL;
-    if (TS > 8) TS = 8;
-    const int j = l / TS, r = l - j * TS;
-    const bool act = j < NL;
-    const int L = act ? j : 0;
-    const Slot sl = lds_slot(sX, nslot, sMeta, L);
-    double ratio_L = e.ratio[0];
+    constexpr int kTS = 64 / (4 * NL) < 8 ? 64 / (4 * NL) : 8;
+    const int jj = l / kTS, r = l - jj * kTS;         // this wave's slot jj (scene 4 w + jj / NL)
+    const int q = 4 * w + jj / NL, L = jj % NL;
+    const bool act = jj < 4 * NL && q < nsc;
+    const int js = l, qs = 4 * w + js / NL;           // the serial steps: one lane per slot
+    const bool act_s = js < 4 * NL && qs < nsc;
+    auto geom = [&](int qq, int LL) {
+        const double* gq = geo + qq * kGeoD;
+        double ratio_L = gq[9];
 #pragma unroll
-    for (int k = 1; k < NL; k++) if (L == k) ratio_L = e.ratio[k];
-    const LaneGeom g = lane_geom_from(e.K, pos_x, pos_y, ca_m, sa_m, e.ref_wp, ratio_L, e.ego_d,
-                                      e.ego_speed, e.ego_vd, L);
-    if (act) team_a1(m, in, g, s, L, sl, r, TS);
+        for (int k = 1; k < NL; k++) if (LL == k) ratio_L = gq[9 + k];
+        return lane_geom_from((int)gq[0], gq[1], gq[2], gq[3], gq[4], (int)gq[5], ratio_L, gq[6], gq[7], gq[8], LL);
+    };
+    const Slot sl = lds_slot(sX, nslot, sMeta, act ? q * NL + L : 0);
+    const Slot sls = lds_slot(sX, nslot, sMeta, act_s ? qs * NL + js % NL : 0);
+    if (act) team_a1(m, in, geom(q, L), s0 + q, L, sl, r, kTS);
     wave_sync();
-    const bool act_s = l < NL;                    // the serial steps: one lane per slot
-    const Slot sls = lds_slot(sX, nslot, sMeta, act_s ? l : 0);
-    if (act_s) team_a2(g, sls);
+    if (act_s) team_a2(geom(qs, js % NL), sls);
     wave_sync();
-    if (act) team_a3(sl, r, TS);
+    if (act) team_a3(sl, r, kTS);
     wave_sync();
     if (act_s) team_a4(sls);
     wave_sync();
-    if (act) team_a5(sl, r, TS);
+    if (act) team_a5(sl, r, kTS);
 }
 
-__device__ __forceinline__ void frame_step_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
-                                                const PrepV& pv, const pp_result& out, int SPB, double* rec,
-                                                uint64_t* adjm) {
+// block g: scenes [g SPB, g SPB + nsc), SPB <= kThreads / 32: the first half of the block runs K1
+// (16 lanes per scene), the second half phase A (4 scenes per wave)
+template <int kThreads>
+__device__ __forceinline__ void wave_step_body(MapG mg, const pp_scene_batch& in, const pp_params& P,
+                                               const PrepV& pv, const pp_result& out, int SPB, double* rec,
+                                               uint64_t* adjm, double* geo) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int n = mg.n;
+    const int64_t g = blockIdx.x, s0 = g * SPB;
+    const int nsc = (int)(in.n_scenes - s0 < SPB ? in.n_scenes - s0 : SPB);
 #ifdef PP_TRACE
-    if (threadIdx.x == 0) {
-        trace_at(kTraceK1 - 1, 0);
-        g_trace[8 * (kTraceK1 - 3) + 0] = wall_clock64();
-        g_trace[8 * (kTraceK1 - 3) + 1] = clock64();
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) trace_at(kTraceK1 - 1, 0);
 #endif
     stage_map(sm, mg.buf, kMapArrays * n);
     __syncthreads();
     const MapV m = map_view(sm, n, mg.fastm);
     double* csm = sm + ((kMapArrays * n + 1) & ~1);
-    if (threadIdx.x < 16) {                       // K1 of scene 0 (16 lanes of the first wave)
+    const int tid = (int)threadIdx.x;
+    if (tid < kThreads / 2) {                     // K1: scene s0 + tid / 16 by 16 lanes
+        const int q = tid / 16;
         const GroupBits nobits = {nullptr, SPB, 1, nullptr, nullptr};
-        prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, 0, (int)threadIdx.x);
-    } else if (threadIdx.x >= 64 && threadIdx.x < 128) {
-        frame_phase_a(m, in, P, SPB, csm, (int)threadIdx.x - 64);
+        if (q < nsc) prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, s0 + q, tid % 16);
+    } else {
+        wave_phase_a(m, in, P, SPB, csm, geo, s0, nsc, (tid - kThreads / 2) / 64, tid % 64);
 #ifdef PP_TRACE
-        if (threadIdx.x == 64) trace_at(kTraceK1 - 4, 0);
+        if (blockIdx.x == 0 && tid == kThreads / 2) trace_at(kTraceK1 - 4, 0);
 #endif
     }
     __syncthreads();
 #ifdef PP_TRACE
-    if (threadIdx.x == 0) trace_at(kTraceK1 - 1, 1);
+    if (blockIdx.x == 0 && tid == 0) trace_at(kTraceK1 - 1, 1);
 #endif
     const MapG ml = {sm, n, mg.fastm};
-    cand_group<false, 1, kStepEmit, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, 0, csm);
+    cand_group<false, 1, kStepEmit, true>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
     __syncthreads();
 #ifdef PP_TRACE
-    if (threadIdx.x == 0) trace_at(kTraceK1 - 1, 2);
+    if (blockIdx.x == 0 && tid == 0) trace_at(kTraceK1 - 1, 2);
 #endif
-    cand_group<true, 1, kStepEmit>(ml, in, P, pv, out, SPB, 1, rec, adjm, 0, csm);
+    cand_group<true, 1, kStepEmit>(ml, in, P, pv, out, SPB, 1, rec, adjm, g, csm);
 #ifdef PP_TRACE
-    if (threadIdx.x == 0) {
-        trace_at(kTraceK1 - 1, 3);
-        g_trace[8 * (kTraceK1 - 3) + 2] = wall_clock64();
-        g_trace[8 * (kTraceK1 - 3) + 3] = clock64();
-    }
+    if (blockIdx.x == 0 && tid == 0) trace_at(kTraceK1 - 1, 3);
 #endif
 }
 
+// waves (host: step_waves_on): the block runs wave_step_body (SPB <= kStepWaveSpb, 256 threads, the
+// geometry records in LDS after k_cand's)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small(
         MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
+        uint64_t* adjm, int waves) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (waves) {                                  // (launch-uniform)
+        double* geo = sm + ((kMapArrays * mg.n + 1) & ~1) + cand_lds_doubles(SPB);
+        wave_step_body<256>(mg, in, P, pv, out, SPB, rec, adjm, geo);
+    } else {
+        step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+    }
+}
+
+// 512 threads: blocks of 16 scenes, K1 on waves 0-3 beside phase A on waves 4-7 (BASELINE config 2:
+// 256 such blocks, one per CU)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_step_small512(
+        MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
         uint64_t* adjm) {
-    step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* geo = sm + ((kMapArrays * mg.n + 1) & ~1) + cand_lds_doubles(SPB);
+    wave_step_body<512>(mg, in, P, pv, out, SPB, rec, adjm, geo);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2509,9 +2558,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 // each field's range out to whole units and merges neighbours): one 16-B load per unit, since
 // the reads cross PCIe as one transaction per load.
 // ------------------------------------------------------------------------------------------------
-#ifndef PP_FRAME_WAVES
-#define PP_FRAME_WAVES 1      // phase A on the block's second wave, beside K1 (frame_step_body)
-#endif
 constexpr int kFioMax = 16;
 constexpr int kFioInline = 176;   // 16-B units of input carried in the kernel arguments (2.75 KB)
 struct FrameIO {
@@ -2558,7 +2604,7 @@ __device__ __forceinline__ void frame_copy(const uint4* __restrict__ src, uint4*
 constexpr size_t kFioArgOff = 0;
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_plan_frame(
         FrameIO io, MapG mg, pp_scene_batch in, pp_params P, PrepV pv, pp_result out, int SPB, double* rec,
-        uint64_t* adjm) {
+        uint64_t* adjm, int waves) {
 #ifdef PP_FRAME_PROF
     const uint64_t t_in = wall_clock64();
 #endif
@@ -2579,11 +2625,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #ifdef PP_FRAME_PROF
     const uint64_t t_body = wall_clock64();
 #endif
-#if PP_FRAME_WAVES
-    frame_step_body(mg, in, P, pv, out, SPB, rec, adjm);
-#else
-    step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
-#endif
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    if (waves) {
+        double* geo = sm + ((kMapArrays * mg.n + 1) & ~1) + cand_lds_doubles(SPB);
+        wave_step_body<256>(mg, in, P, pv, out, SPB, rec, adjm, geo);
+    } else {
+        step_small_body(mg, in, P, pv, out, SPB, rec, adjm);
+    }
     __threadfence_block();
     __syncthreads();
 #ifdef PP_FRAME_PROF
@@ -3020,17 +3068,30 @@ bool split_on(int64_t S) {
 // scenes: 2.07 ms for 32,768 waves at 3, 2.29 ms at 4); 262,144 scenes (BASELINE config 5 over 8
 // GPUs) = 4,096 waves = 1.33 rounds at 3 (0.352 ms measured) or exactly 1 at 4. PP_DBG_PREP_WAVES
 // forces 3 or 4.
-bool prep_w4(int64_t Sv, int device) {
-    const int f = dbg(PP_DBG_PREP_WAVES);
-    if (f == 3 || f == 4) return f == 4;
+int cu_count(int device) {
     static int cus[kMaxDev] = {};
-    if (device < 0 || device >= kMaxDev) return false;
+    if (device < 0 || device >= kMaxDev) return 256;
     if (cus[device] == 0) {
         int c = 0;
         if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c <= 0) c = 256;
         cus[device] = c;
     }
-    const int64_t waves = (Sv + 63) / 64, simds = 4LL * cus[device];
+    return cus[device];
+}
+// the one-launch step with phase A beside K1 (wave_step_body) where its blocks fit one per CU:
+// 8-scene blocks of 256 threads (the frame, batches up to 2,048 scenes: 0.128 -> 0.116 ms at 2,048),
+// else 16-scene blocks of 512 threads; beyond, 16-scene blocks of 256 threads, K1 then phase A
+// (2 blocks of 8 per CU measured slower: config 2 0.132 against 0.128 ms, profiles/r04_ablations.txt)
+int step_waves_on(int64_t S, int spb, int device) {
+    if (!kStepWaves) return 0;
+    if ((S + kStepWaveSpb - 1) / kStepWaveSpb <= cu_count(device)) return 1;
+    if (spb >= 16 && (S + 15) / 16 <= cu_count(device)) return 2;
+    return 0;
+}
+bool prep_w4(int64_t Sv, int device) {
+    const int f = dbg(PP_DBG_PREP_WAVES);
+    if (f == 3 || f == 4) return f == 4;
+    const int64_t waves = (Sv + 63) / 64, simds = 4LL * cu_count(device);
     const int64_t r3 = (waves + 3 * simds - 1) / (3 * simds), r4 = (waves + 4 * simds - 1) / (4 * simds);
     return 286 * r4 < 188 * r3;
 }
@@ -3370,10 +3431,19 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                        fused_small(S);
     const bool emit_in = fused;
     // small reference-mode batches with the map in LDS: the whole step in one launch (k_step_small)
-    const int spb_f = std::min(cg.spb, 256 / 16);
-    const int64_t groups_f = (S + spb_f - 1) / spb_f;
+    // (kStepWaves: blocks of up to kStepWaveSpb scenes in 256 threads, K1 and phase A side by side,
+    // plus the per-scene geometry records; otherwise up to 16 scenes, K1 then phase A)
+    // step_waves: 1 blocks of 8 scenes in 256 threads, 2 blocks of 16 scenes in 512 threads, 0 the
+    // 16-scene blocks without the split
+    int step_waves = step_waves_on(S, cg.spb, device);
     const size_t map_lds = sizeof(double) * (size_t)((kMapArrays * M->n + 1) & ~1);
-    const size_t lds_f = map_lds + cand_geom_lds(spb_f);
+    auto step_lds = [&](int wv, int spb) {
+        return map_lds + (wv != 0 ? sizeof(double) * (size_t)(cand_lds_doubles(spb) + kGeoD * spb) : cand_geom_lds(spb));
+    };
+    if (step_waves && step_lds(step_waves, std::min(cg.spb, step_waves == 1 ? kStepWaveSpb : 16)) > 65536) step_waves = 0;
+    const int spb_f = std::min(cg.spb, step_waves == 1 ? kStepWaveSpb : 256 / 16);
+    const int64_t groups_f = (S + spb_f - 1) / spb_f;
+    const size_t lds_f = step_lds(step_waves, spb_f);
     const bool step_fused = fused && M->n <= kLdsMapMax && lds_f <= 65536 && step_fused_on();
     if (fio && (!step_fused || groups_f != 1)) return PP_ERR_STATE;
     // the map lock is held from workspace binding through the (asynchronous) launches: a
@@ -3464,13 +3534,17 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
         // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
-        const int threads_f = std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
+        const int threads_f = step_waves == 1 ? 256 : step_waves == 2 ? 512
+                                                      : std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
         if (fio) {
             hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, *fio, mg, B, P, pv, R, spb_f,
-                               rec, adjm);
+                               rec, adjm, step_waves == 1 ? 1 : 0);
+        } else if (step_waves == 2) {
+            hipLaunchKernelGGL(k_step_small512, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P,
+                               pv, R, spb_f, rec, adjm);
         } else {
             hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
-                               R, spb_f, rec, adjm);
+                               R, spb_f, rec, adjm, step_waves == 1 ? 1 : 0);
         }
         if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
