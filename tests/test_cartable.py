@@ -206,6 +206,15 @@ class TestCarTableGPU:
               f"with erased {erased}, max reported {rep}")
         assert (stale if need == "stale" else erased) > 0
 
+    @pytest.mark.parametrize("shape", [ppamd.SHAPE_SPLIT, ppamd.SHAPE_CAND_SMALL, ppamd.SHAPE_STEP])
+    def test_plan_frame_episode_other_shapes(self, env, shape):
+        """pp_plan_frame under a forced launch shape: the split and cand_small shapes leave the
+        one-launch frame kernel (k_plan_frame) for its fallback, copies + pp_eval; every shape
+        must give the reference's frames (30 cars, ids >= 16, stale entries)."""
+        with ppamd.debug(ppamd.DBG_SHAPE, shape):
+            worst, stale, erased, rep = run_episode(env, list(range(16, 46)), 80, 12, 1e5)
+        assert rep > 25                                  # beyond the kernel-argument inputs too
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("S", [37, 5000])
