@@ -4202,7 +4202,9 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
                 if (e == hipSuccess && *flag != io.seq) { rc = PP_ERR_HIP; break; }
                 if (e != hipSuccess && e != hipErrorNotReady) { rc = PP_ERR_HIP; break; }
             }
+#if defined(__x86_64__) || defined(__i386__)
             __builtin_ia32_pause();
+#endif
         }
         std::atomic_thread_fence(std::memory_order_acquire);
 #ifdef PP_FRAME_PROF

@@ -31,4 +31,8 @@ run bench_config4_montecarlo --draws 64 --n-speeds 1 --scenes 16384 --no-cpu-bas
 run bench_shard_262144 --scenes 262144 --no-cpu-baseline --no-pcie
 run bench_rollout_2M_x10 --rollout 10 --no-cpu-baseline --no-pcie
 timeout -k 10 300 python3 tools/split_probe.py 262144 2 > $OUT/split_probe.txt 2>&1; tail -4 $OUT/split_probe.txt
+timeout -k 10 300 python3 tools/split_probe.py 524288 2 > $OUT/split_probe_524288.txt 2>&1; tail -4 $OUT/split_probe_524288.txt
 timeout -k 10 200 python3 tools/bench_frame.py --frames 2000 > $OUT/frame.json 2> $OUT/frame.err; cat $OUT/frame.json
+L=$PWD/carnd-path-planning-project_amd/ppamd
+PPAMD_LIB=$L/libppamd_var_fprof.so timeout -k 10 120 python3 tools/frame_prof.py > $OUT/frame_prof.json 2>&1; tail -1 $OUT/frame_prof.json
+PPAMD_LIB=$L/libppamd_var_trace.so timeout -k 10 120 python3 tools/trace_frame.py > $OUT/trace_frame.json 2>&1; tail -1 $OUT/trace_frame.json
