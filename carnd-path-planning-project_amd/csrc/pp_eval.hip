@@ -2836,6 +2836,13 @@ constexpr int kPrepI = 7;
 // pp_eval's device workspaces, one set per HIP stream: evaluations on different streams never
 // share intermediate buffers, and evaluations on one stream are ordered by it. A buffer is grown
 // only after that stream has drained (it is the only stream using it).
+// the split of shard-sized batches: parts (streams) per call, at most kSplitMax
+constexpr int kSplitMax = 4;
+#ifndef PP_SPLIT_PARTS
+#define PP_SPLIT_PARTS 2
+#endif
+constexpr int kSplitParts = PP_SPLIT_PARTS;
+static_assert(kSplitParts >= 2 && kSplitParts <= kSplitMax, "split parts");
 struct StreamWS {
     void* ws = nullptr;           // prep workspace (per evaluation: scene x draw)
     int64_t ws_cap = 0;
@@ -2843,8 +2850,8 @@ struct StreamWS {
     int64_t rec_cap = 0;
     uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
     int64_t gbits_cap = 0;        // words
-    hipStream_t st2 = nullptr;    // the two-stream split's second stream (shard-sized batches)
-    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t st2[kSplitMax - 1] = {};   // the split's other streams (shard-sized batches)
+    hipEvent_t fork = nullptr, join[kSplitMax - 1] = {};
 };
 struct DevState {
     bool init = false;
@@ -2864,10 +2871,10 @@ struct DevState {
     pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
     bool timing = false;          // pp_timing_enable
     std::vector<hipEvent_t> ev_pool;
-    // groups of 8 per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch stream (the
-    // two-stream split: those four per half, each half's on its own stream, events 4-7 the second's)
+    // groups of 4 kSplitMax per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch
+    // stream (the split: those four per part, each part's on its own stream, events 4 h .. 4 h + 3)
     std::vector<hipEvent_t> ev_rec;
-    std::vector<int> ev_kind;     // per group: bit 0 K3/K4 launched, bit 1 two-stream split
+    std::vector<int> ev_kind;     // per group: bit 0 K3/K4 launched, bits 1-3 the split's parts (0: none)
 };
 
 }  // namespace
@@ -3057,11 +3064,11 @@ bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // (262,144 scenes) run as two halves, each K1 -> K2 -> K4 on its own stream, so one half's kernels
 // fill the other's start-up and tail (a batch this size is ~15 rounds of k_cand blocks and one of
 // k_prep waves). PP_DBG_SPLIT 1 forces it (any split-eligible batch), 2 off.
-constexpr int64_t kSplitMin = 131072, kSplitMax = 786432;
+constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 786432;
 bool split_on(int64_t S) {
     const int f = dbg(PP_DBG_SPLIT);
     if (f == 2) return false;
-    return f == 1 ? S >= 2048 : (S >= kSplitMin && S <= kSplitMax);
+    return f == 1 ? S >= 2048 : (S >= kSplitMin && S <= kSplitMaxScenes);
 }
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
 // 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
@@ -3155,7 +3162,7 @@ int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
     // [bits: cap words][flagged-group count][the split's second-half count][list: 32 cap entries]
-    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + 2 + 32 * cap);
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + kSplitMax + 32 * cap);
     if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
@@ -3163,9 +3170,11 @@ int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
 }
 
 void free_ws(StreamWS& W) {
-    if (W.st2) (void)hipStreamDestroy(W.st2);
+    for (int k = 0; k < kSplitMax - 1; k++) {
+        if (W.st2[k]) (void)hipStreamDestroy(W.st2[k]);
+        if (W.join[k]) (void)hipEventDestroy(W.join[k]);
+    }
     if (W.fork) (void)hipEventDestroy(W.fork);
-    if (W.join) (void)hipEventDestroy(W.join);
     if (W.ws) (void)hipFree(W.ws);
     if (W.rec) (void)hipFree(W.rec);
     if (W.gbits) (void)hipFree(W.gbits);
@@ -3480,7 +3489,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             if (w) return PP_ERR_STATE;
         const bool ok = fill(W.ws, prep_bytes(W.ws_cap)) &&
                         fill(W.rec, W.rec ? rec_bytes(W.rec_cap) : 0) &&
-                        fill(W.gbits + W.gbits_cap + 2, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
+                        fill(W.gbits + W.gbits_cap + kSplitMax, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
                         fill(out->winner, 4 * S) && fill(out->n_out, 4 * S) && fill(out->status, 4 * S) &&
                         fill(out->next_x, 8 * N * S) && fill(out->next_y, 8 * N * S) &&
                         fill(out->cost, 8 * Cn * S) && fill(out->info, sizeof(pp_scene_info) * S) &&
@@ -3494,10 +3503,10 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.buf = DS.map;
     mg.n = M->n;
     mg.fastm = M->fastm;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[4 * kSplitMax] = {};
     const bool timing = DS.timing;
     if (timing) {
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < 4 * kSplitMax; i++) {
             if (DS.ev_pool.empty()) {
                 hipEvent_t e;
                 if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
@@ -3516,7 +3525,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     GroupBits gb;
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     gb.count = W.gbits + W.gbits_cap;
-    gb.list = gb.count + 2;
+    gb.list = gb.count + kSplitMax;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -3550,58 +3559,62 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
-    if (hipMemsetAsync(gb.count, 0, 2 * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
+    if (hipMemsetAsync(gb.count, 0, kSplitMax * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     const bool split = ref_direct && !P.emit_paths && !fused && cg.bps == 1 && Dn == 1 &&
                        prep_group(Sv) == 1 && split_on(S);
     if (split) {
-        // halves at a group boundary: groups [0, ga) (scenes [0, sa)) on the caller's stream,
-        // [ga, G) on the second; each half its own flagged-group list (count words 0 and 1, the
-        // second half's list after the first half's ga entries). Timing: each half's kernels by
-        // events on its own stream (two launches of each kernel per call; they overlap the other
-        // half's, as in a rocprofv3 kernel trace of the same call).
-        if (!W.st2) {
-            if (hipStreamCreateWithFlags(&W.st2, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&W.join, hipEventDisableTiming) != hipSuccess)
-                return PP_ERR_HIP;
+        // kSplitParts parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
+        // their scenes, part 0 on the caller's stream, part h > 0 on stream st2[h - 1]; each part
+        // its own flagged-group list (count word h, its list from its first group's index on).
+        // Timing: each part's kernels by events on its own stream (P launches of each kernel per
+        // call; they overlap the other parts', as in a rocprofv3 kernel trace of the same call).
+        const int NP = kSplitParts;
+        if (!W.fork) {
+            if (hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
+            for (int k = 0; k < NP - 1; k++)
+                if (hipStreamCreateWithFlags(&W.st2[k], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&W.join[k], hipEventDisableTiming) != hipSuccess)
+                    return PP_ERR_HIP;
         }
-        const int64_t G = cg.groups, ga = G / 2, sa = std::min<int64_t>(S, ga * cg.spb);
-        GroupBits gbh[2] = {gb, gb};
-        gbh[1].count = gb.count + 1;
-        gbh[1].list = gb.list + ga;
-        if (timing) DS.ev_kind.back() |= 2;
-        if (hipEventRecord(W.fork, st) != hipSuccess || hipStreamWaitEvent(W.st2, W.fork, 0) != hipSuccess)
-            return PP_ERR_HIP;
+        const int64_t G = cg.groups;
+        if (timing) DS.ev_kind.back() |= NP << 1;
+        if (hipEventRecord(W.fork, st) != hipSuccess) return PP_ERR_HIP;
+        for (int k = 0; k < NP - 1; k++)
+            if (hipStreamWaitEvent(W.st2[k], W.fork, 0) != hipSuccess) return PP_ERR_HIP;
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
-        for (int h = 0; h < 2; h++) {
-            hipStream_t sh = h == 0 ? st : W.st2;
-            const int64_t v0 = h == 0 ? 0 : sa, v1 = h == 0 ? sa : S;
-            const int64_t g0 = h == 0 ? 0 : ga, g1 = h == 0 ? ga : G;
+        for (int h = 0; h < NP; h++) {
+            hipStream_t sh = h == 0 ? st : W.st2[h - 1];
+            const int64_t g0 = G * h / NP, g1 = G * (h + 1) / NP;
+            const int64_t v0 = std::min<int64_t>(S, g0 * cg.spb), v1 = std::min<int64_t>(S, g1 * cg.spb);
             if (v1 <= v0) continue;     // (never: the split takes batches of >= 2,048 scenes)
+            GroupBits gbh = gb;
+            gbh.count = gb.count + h;
+            gbh.list = gb.list + g0;
             hipEvent_t* eh = ev + 4 * h;
             if (timing) (void)hipEventRecord(eh[0], sh);
             const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
             if (prep_w4(v1 - v0, device)) {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             } else {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh[h], v0, v1);
+                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             }
             if (timing) (void)hipEventRecord(eh[1], sh);
             const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
             hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
-                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
+                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
             hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
-                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh[h].list, gbh[h].count, g0);
+                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
             if (timing) (void)hipEventRecord(eh[2], sh);
             hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
                                rec, adjm, v0, v1);
             if (timing) (void)hipEventRecord(eh[3], sh);
         }
-        if (hipEventRecord(W.join, W.st2) != hipSuccess || hipStreamWaitEvent(st, W.join, 0) != hipSuccess)
-            return PP_ERR_HIP;
+        for (int k = 0; k < NP - 1; k++)
+            if (hipEventRecord(W.join[k], W.st2[k]) != hipSuccess || hipStreamWaitEvent(st, W.join[k], 0) != hipSuccess)
+                return PP_ERR_HIP;
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
@@ -3712,7 +3725,7 @@ int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
         DeviceGuard g(device);
         const int rc = dev_init(M, device);       // (pp_map_destroy frees the events of initialised devices)
         if (rc) return rc;
-        while (D.ev_pool.size() + D.ev_rec.size() < 8 * 256) {
+        while (D.ev_pool.size() + D.ev_rec.size() < 4 * kSplitMax * 256) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
             D.ev_pool.push_back(e);
@@ -3728,11 +3741,12 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     DeviceGuard g(device);
     for (int k = 0; k < 3; k++) { ms3[k] = 0; launches3[k] = 0; }
     int rc = PP_OK;
-    const size_t ng = D.ev_rec.size() / 8;
+    constexpr int EG = 4 * kSplitMax;
+    const size_t ng = D.ev_rec.size() / EG;
     for (size_t i = 0; i < ng; i++) {
-        const int kind = D.ev_kind[i];
-        for (int h = 0; h < ((kind & 2) ? 2 : 1); h++) {
-            hipEvent_t* e = &D.ev_rec[8 * i + 4 * h];
+        const int kind = D.ev_kind[i], parts = (kind >> 1) & 7;
+        for (int h = 0; h < (parts ? parts : 1); h++) {
+            hipEvent_t* e = &D.ev_rec[EG * i + 4 * h];
             if (hipEventSynchronize(e[3]) != hipSuccess) rc = PP_ERR_HIP;
             float t;
             if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
@@ -3741,7 +3755,7 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
                 if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
             }
         }
-        for (int k = 0; k < 8; k++) D.ev_pool.push_back(D.ev_rec[8 * i + k]);
+        for (int k = 0; k < EG; k++) D.ev_pool.push_back(D.ev_rec[EG * i + k]);
     }
     D.ev_rec.clear();
     D.ev_kind.clear();

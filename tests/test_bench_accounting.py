@@ -64,3 +64,46 @@ def test_workload_names():
     assert w(2097152, 15, 5, 50, False, 1, 0) == "BASELINE config 5"
     assert w(262144, 15, 5, 50, False, 1, 0) == "BASELINE config 5"     # a shard of it
     assert w(65536, 15, 5, 50, False, 1, 100).startswith("closed-loop")
+
+
+def test_rocprof_summary_entries():
+    """profiles/rocprof_summary.json (tools/rocprof_summarize.py): every entry names its launch shape
+    and its K2 launches per step (2 where pp_eval splits a shard over two streams), the candidates
+    of one launch are the shape's divided by those launches, and the recomputed fraction of HBM peak
+    is the one a bench line of that shape reports as roofline.frac_rocprof."""
+    rp = bench.load_rocprof_all()
+    assert rp, "profiles/rocprof_summary.json missing"
+    for tag, e in rp.items():
+        lps = e["launches_per_step"]
+        assert lps in (1, 2, 3, 4), tag
+        assert e["candidates_per_launch"] == e["scenes"] * e["candidates_per_scene"] // lps, tag
+        assert bench.pmc_tag(e["scenes"], e["candidates_per_scene"], e["n_points"], e["emit_paths"],
+                             e.get("draws", 1)) == tag
+        assert 0 < e["dominant_ms_per_launch"] < 100, tag
+        bpc = bench.algorithmic_bytes_per_candidate(e["candidates_per_scene"], e["n_points"], e["emit_paths"])
+        frac = bpc * e["candidates_per_launch"] / (e["dominant_ms_per_launch"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS
+        assert 0 < frac < 1, tag
+    # the shard is split in two: its entry says so
+    assert rp["k_cand_S262144_C15_N50"]["launches_per_step"] == 2
+
+
+def test_rocprof_summarize_tool(tmp_path):
+    """tools/rocprof_summarize.py on a synthetic kernel-stats CSV: the dominant kernel's time per
+    launch sums both k_cand instantiations per dispatch, the other kernels are listed."""
+    import subprocess
+    import sys
+    d = tmp_path / "stats" / "host"
+    d.mkdir(parents=True)
+    rows = ['"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"',
+            '"void k_cand<false, 1>(MapG, pp_scene_batch)",26,26000000,1000000.0,70,1,1,0',
+            '"void k_cand<true, 1>(MapG, pp_scene_batch)",26,260000,10000.0,1,1,1,0',
+            '"void k_prep<true, false>(MapG)",26,5200000,200000.0,20,1,1,0']
+    (d / "run_kernel_stats.csv").write_text("\n".join(rows) + "\n")
+    (tmp_path / "profiles").mkdir()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "rocprof_summarize.py"), str(tmp_path / "stats"),
+                        "k_cand_S262144_C15_N50", "2"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = json.load(open(tmp_path / "profiles" / "rocprof_summary.json"))["k_cand_S262144_C15_N50"]
+    assert out["dominant_ms_per_launch"] == pytest.approx(1.01)
+    assert out["launches_per_step"] == 2 and out["candidates_per_launch"] == 262144 * 15 // 2
+    assert "k_prep<true, false>" in out["kernels"]
