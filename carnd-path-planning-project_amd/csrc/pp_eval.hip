@@ -318,7 +318,7 @@ __device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_
 // kLimSlow scene in this bitmap for k_cand<true>
 // (list/count: the flagged groups in the order k_prep found them, for k_cand<true>; count is zeroed
 // before every K1)
-struct GroupBits { uint32_t* bits; int SPB, BPS; uint32_t* list; uint32_t* count; };
+struct GroupBits { uint32_t* bits; int SPB, BPS; uint32_t* list; uint32_t* count; int pose_by_wave; };
 // ---- K1 building blocks, shared by k_prep (one lane per evaluation) and k_prep_g2..16 (G lanes) ----
 
 // Ego state of one evaluation: derivation (src/main.cpp:1233-1292), Frenet frame and ego matching
@@ -724,11 +724,15 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
         ok = grp_or<G>(ok ? 0u : 1u) == 0u;
     }
     // TrajectoryBuilder::build start pose (src/main.cpp:583-610) + frame rotations (:786-823)
-    double pos_x, pos_y, angle;
-    start_pose(in, S, s, e, pos_x, pos_y, angle);
-    // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
-    // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
-    if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
+    // (gb.pose_by_wave: the wave step's phase-A waves compute and record the start pose, its
+    // rotations and the heading's kLimSlow bit themselves, off K1's critical path)
+    double pos_x = 0, pos_y = 0, angle = 0;
+    if (!gb.pose_by_wave) {
+        start_pose(in, S, s, e, pos_x, pos_y, angle);
+        // heading beyond the hot loop's medium trig range (only from an absurd telemetry yaw): the
+        // scene is evaluated by the k_cand<true> instantiation with the library's large reduction
+        if (!(fabs(angle) <= kSlowAngle)) lim_mask |= kLimSlow;
+    }
     if (!ok) lim_mask |= kLimSlow;
     if ((lim_mask & kLimSlow) && r == 0 && gb.bits) {   // (k_step_small: no bitmap)
         const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
@@ -742,14 +746,16 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     // (:822-823) as the reference's libm computes them (pp_glibcm.h): every knot is a product with
     // them, so the spline and every path position carry their exact bits. Headings of 1e8 rad and
     // more (only from an absurd telemetry yaw) are outside the restated reduction.
-    double tv[4];
-    frame_trig<G>(angle, r, tv);
-    double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
+    if (!gb.pose_by_wave) {
+        double tv[4];
+        frame_trig<G>(angle, r, tv);
+        double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-        if (G == 1 || t % G == r) tdst[t][v] = tv[t];
+        for (int t = 0; t < 4; t++)
+            if (G == 1 || t % G == r) tdst[t][v] = tv[t];
+        if (r == 0) { pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle; }
+    }
     if (r != 0) return;
-    pv.pos_x[v] = pos_x; pv.pos_y[v] = pos_y; pv.angle[v] = angle;
     pv.ego_speed[v] = e.ego_speed; pv.ego_d[v] = e.ego_d; pv.ego_vd[v] = e.ego_vd;
 #pragma unroll
     for (int l = 0; l < NL; l++) { pv.ratio[l * Sv + v] = e.ratio[l]; pv.score[l * Sv + v] = score[l]; }
@@ -2420,8 +2426,12 @@ __device__ __forceinline__ void step_small_body(MapG mg, const pp_scene_batch& i
 // by wave (one instruction stream; LDS is in order within a wave), the per-scene geometry passing
 // through an LDS record of kGeoD doubles per scene.
 constexpr int kStepWaveSpb = 8;
-constexpr int kGeoD = 16;
-static_assert(10 + NL <= kGeoD, "geometry record");
+constexpr int kGeoD = 17;           // (the last: the heading)
+static_assert(9 + NL <= kGeoD - 1, "geometry record");
+#ifndef PP_POSE_BY_WAVE
+#define PP_POSE_BY_WAVE 1
+#endif
+constexpr bool kPoseByWave = PP_POSE_BY_WAVE != 0;
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2429,7 +2439,8 @@ __device__ __forceinline__ void wave_sync() {
 }
 // wave w of the phase-A waves, lane l: scenes [4 w, 4 w + 4) of the block's nsc
 __device__ __forceinline__ void wave_phase_a(const MapV& m, const pp_scene_batch& in, const pp_params& P,
-                                             int SPB, double* sm, double* geo, int64_t s0, int nsc, int w, int l) {
+                                             const PrepV& pv, int SPB, double* sm, double* geo, int64_t s0,
+                                             int nsc, int w, int l) {
     const int64_t S = in.n_scenes;
     {   // the ego state, start pose and rotations of scene q by 16 lanes; lane 0 records them
         const int q = 4 * w + l / 16, r = l % 16;
@@ -2442,8 +2453,15 @@ __device__ __forceinline__ void wave_phase_a(const MapV& m, const pp_scene_batch
             double tv[4];
             frame_trig<16>(angle, r, tv);
             const double ca_m = __shfl(tv[0], 0, 16), sa_m = __shfl(tv[1], 1, 16);
+            // the prep record's pose and rotations (K1 skips them: GroupBits.pose_by_wave)
+            double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (t == r) tdst[t][s] = tv[t];
+            if (r == 0) { pv.pos_x[s] = pos_x; pv.pos_y[s] = pos_y; pv.angle[s] = angle; }
             if (r == 0) {
                 double* gq = geo + q * kGeoD;
+                gq[kGeoD - 1] = angle;
                 gq[0] = e.K; gq[1] = pos_x; gq[2] = pos_y; gq[3] = ca_m; gq[4] = sa_m; gq[5] = e.ref_wp;
                 gq[6] = e.ego_d; gq[7] = e.ego_speed; gq[8] = e.ego_vd;
 #pragma unroll
@@ -2501,15 +2519,19 @@ __device__ __forceinline__ void wave_step_body(MapG mg, const pp_scene_batch& in
     const int tid = (int)threadIdx.x;
     if (tid < kThreads / 2) {                     // K1: scene s0 + tid / 16 by 16 lanes
         const int q = tid / 16;
-        const GroupBits nobits = {nullptr, SPB, 1, nullptr, nullptr};
+        const GroupBits nobits = {nullptr, SPB, 1, nullptr, nullptr, kPoseByWave ? 1 : 0};
         if (q < nsc) prep_grp_eval<16>(m, in, P, pv, out.info, out.status, nobits, s0 + q, tid % 16);
     } else {
-        wave_phase_a(m, in, P, SPB, csm, geo, s0, nsc, (tid - kThreads / 2) / 64, tid % 64);
+        wave_phase_a(m, in, P, pv, SPB, csm, geo, s0, nsc, (tid - kThreads / 2) / 64, tid % 64);
 #ifdef PP_TRACE
         if (blockIdx.x == 0 && tid == kThreads / 2) trace_at(kTraceK1 - 4, 0);
 #endif
     }
     __syncthreads();
+    // the heading's kLimSlow bit (recorded by the phase-A waves), before cand_group's first read
+    // of lim_mask (behind its first barrier)
+    if (kPoseByWave && tid < nsc && !(fabs(geo[tid * kGeoD + kGeoD - 1]) <= kSlowAngle))
+        pv.lim_mask[s0 + tid] |= kLimSlow;
 #ifdef PP_TRACE
     if (blockIdx.x == 0 && tid == 0) trace_at(kTraceK1 - 1, 1);
 #endif
@@ -2836,13 +2858,11 @@ constexpr int kPrepI = 7;
 // pp_eval's device workspaces, one set per HIP stream: evaluations on different streams never
 // share intermediate buffers, and evaluations on one stream are ordered by it. A buffer is grown
 // only after that stream has drained (it is the only stream using it).
-// the split of shard-sized batches: parts (streams) per call, at most kSplitMax
+// the split of shard-sized batches: parts (streams) per call, at most kSplitMax (split_parts)
 constexpr int kSplitMax = 4;
 #ifndef PP_SPLIT_PARTS
-#define PP_SPLIT_PARTS 2
+#define PP_SPLIT_PARTS 0      // 0: by batch size (split_parts); 2..4 forced (A/B builds)
 #endif
-constexpr int kSplitParts = PP_SPLIT_PARTS;
-static_assert(kSplitParts >= 2 && kSplitParts <= kSplitMax, "split parts");
 struct StreamWS {
     void* ws = nullptr;           // prep workspace (per evaluation: scene x draw)
     int64_t ws_cap = 0;
@@ -3069,6 +3089,13 @@ bool split_on(int64_t S) {
     const int f = dbg(PP_DBG_SPLIT);
     if (f == 2) return false;
     return f == 1 ? S >= 2048 : (S >= kSplitMin && S <= kSplitMaxScenes);
+}
+// parts of a split batch: 2 up to 393,216 scenes (BASELINE config 5's N = 8 shard, 262,144: 1.32 ms
+// against 1.35 / 1.37 ms with 3 / 4 parts), 3 beyond (its N = 4 shard, 524,288: 2.52 ms against
+// 2.59-2.62 with 2 parts and 2.60 unsplit; profiles/r04_ablations.txt)
+int split_parts(int64_t S) {
+    if (PP_SPLIT_PARTS >= 2 && PP_SPLIT_PARTS <= kSplitMax) return PP_SPLIT_PARTS;
+    return S > 393216 ? 3 : 2;
 }
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
 // 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
@@ -3522,7 +3549,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     pp_scene_batch B = *in;
     pp_result R = *out;
     if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
-    GroupBits gb;
+    GroupBits gb = {};
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
     gb.count = W.gbits + W.gbits_cap;
     gb.list = gb.count + kSplitMax;
@@ -3563,19 +3590,17 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     const bool split = ref_direct && !P.emit_paths && !fused && cg.bps == 1 && Dn == 1 &&
                        prep_group(Sv) == 1 && split_on(S);
     if (split) {
-        // kSplitParts parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
+        // split_parts(S) parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
         // their scenes, part 0 on the caller's stream, part h > 0 on stream st2[h - 1]; each part
         // its own flagged-group list (count word h, its list from its first group's index on).
         // Timing: each part's kernels by events on its own stream (P launches of each kernel per
         // call; they overlap the other parts', as in a rocprofv3 kernel trace of the same call).
-        const int NP = kSplitParts;
-        if (!W.fork) {
-            if (hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
-            for (int k = 0; k < NP - 1; k++)
-                if (hipStreamCreateWithFlags(&W.st2[k], hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&W.join[k], hipEventDisableTiming) != hipSuccess)
-                    return PP_ERR_HIP;
-        }
+        const int NP = split_parts(S);
+        if (!W.fork && hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
+        for (int k = 0; k < NP - 1; k++)
+            if (!W.st2[k] && (hipStreamCreateWithFlags(&W.st2[k], hipStreamNonBlocking) != hipSuccess ||
+                              hipEventCreateWithFlags(&W.join[k], hipEventDisableTiming) != hipSuccess))
+                return PP_ERR_HIP;
         const int64_t G = cg.groups;
         if (timing) DS.ev_kind.back() |= NP << 1;
         if (hipEventRecord(W.fork, st) != hipSuccess) return PP_ERR_HIP;

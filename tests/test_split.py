@@ -1,8 +1,8 @@
-"""The two-stream split (pp_eval, include/pp.h PP_DBG_SPLIT): reference-mode batches of about an
-8-GPU shard's size run as two halves, each K1 -> K2 -> K4 on its own stream. The halves write
-disjoint ranges of every buffer and keep separate flagged-group lists, so the results must be the
-one-stream launch's BIT FOR BIT, including the scenes routed to k_cand<true> and a half boundary
-that splits no group; a sample is checked against the oracle."""
+"""The multi-stream split (pp_eval, include/pp.h PP_DBG_SPLIT): reference-mode batches of about a
+4- or 8-GPU shard's size run as 2 parts (up to 393,216 scenes) or 3 parts, each K1 -> K2 -> K4 on
+its own stream. The parts write disjoint ranges of every buffer and keep separate flagged-group
+lists, so the results must be the one-stream launch's BIT FOR BIT, including the scenes routed to
+k_cand<true> and part boundaries that split no group; a sample is checked against the oracle."""
 import numpy as np
 import pytest
 
@@ -31,7 +31,8 @@ def run(env, sc, prm, mode):
     return ppamd.result_to_numpy(r)
 
 
-@pytest.mark.parametrize("S,mode", [(140000, ppamd.SPLIT_AUTO), (20000, ppamd.SPLIT_ON), (20011, ppamd.SPLIT_ON)])
+@pytest.mark.parametrize("S,mode", [(140000, ppamd.SPLIT_AUTO), (420000, ppamd.SPLIT_AUTO), (20000, ppamd.SPLIT_ON),
+                                    (20011, ppamd.SPLIT_ON)])
 def test_split_bit_identical(env, S, mode):
     sc = ppamd.synth_host(env["m"], S, seed=S, first=S)
     idx = np.arange(7, S, 211)                    # speed-edge scenes: k_cand<true> groups in both halves
@@ -42,7 +43,8 @@ def test_split_bit_identical(env, S, mode):
     for k in a:
         x, y = np.asarray(a[k]), np.asarray(b[k])
         assert (x.view(np.uint8) == y.view(np.uint8)).all(), k
-    sub = np.r_[0:300, S // 2 - 300:S // 2 + 300, S - 300:S]
+    sub = np.unique(np.r_[0:300, S // 3 - 200:S // 3 + 200, S // 2 - 300:S // 2 + 300, 2 * S // 3 - 200:2 * S // 3 + 200,
+                          S - 300:S])
     part = {k: np.ascontiguousarray(v[..., sub]) for k, v in sc.items()}
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], part, prm, info=False)
     got = {k: (v[:, sub] if k in ("next_x", "next_y") else v[sub]) for k, v in a.items()}

@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
-bash tools/gpu_suite.sh $TAG/suite
+[ "${2:-}" = "--no-suite" ] || bash tools/gpu_suite.sh $TAG/suite
 rp() { name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/$name -o run -- python3 $ROOT/bench.py --no-cpu-baseline --no-pcie "$@" > $OUT/$name.json 2> $OUT/$name.err; echo "rocprof $name done"; }
 rp stats5
 rp stats3 --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
