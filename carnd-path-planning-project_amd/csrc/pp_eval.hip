@@ -2889,12 +2889,14 @@ struct DevState {
     void* stage_host = nullptr;   // its pinned host mirror (one copy per direction and region)
     std::mutex stage_mu;          // one pp_plan_batch_host at a time per device
     pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
-    bool timing = false;          // pp_timing_enable
+    int timing = 0;               // pp_timing_enable: 0 off, 1 every kernel, 2 K2 only
     std::vector<hipEvent_t> ev_pool;
     // groups of 4 kSplitMax per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch
     // stream (the split: those four per part, each part's on its own stream, events 4 h .. 4 h + 3)
     std::vector<hipEvent_t> ev_rec;
-    std::vector<int> ev_kind;     // per group: bit 0 K3/K4 launched, bits 1-3 the split's parts (0: none)
+    // per group: bit 0 K3/K4 launched, bits 1-3 the split's parts (0: none), bit 4 K2's events only,
+    // bit 5 no K1 kernel (the one-launch step)
+    std::vector<int> ev_kind;
 };
 
 }  // namespace
@@ -3531,7 +3533,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.n = M->n;
     mg.fastm = M->fastm;
     hipEvent_t ev[4 * kSplitMax] = {};
-    const bool timing = DS.timing;
+    // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two)
+    const bool timing = DS.timing != 0, tall = DS.timing == 1, tk2 = timing;
     if (timing) {
         for (int i = 0; i < 4 * kSplitMax; i++) {
             if (DS.ev_pool.empty()) {
@@ -3543,7 +3546,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             DS.ev_pool.pop_back();
             DS.ev_rec.push_back(ev[i]);
         }
-        DS.ev_kind.push_back(!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0);
+        DS.ev_kind.push_back((!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0) | (tall ? 0 : 16));
     }
     pp_params P = *prm;
     pp_scene_batch B = *in;
@@ -3567,7 +3570,9 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     }
 #endif
     if (step_fused) {
-        if (timing) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
+        if (timing) DS.ev_kind.back() |= 32;          // (no K1 kernel: K1 runs inside the step)
+        if (tall) (void)hipEventRecord(ev[0], st);
+        if (tk2) (void)hipEventRecord(ev[1], st);
         // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
         const int threads_f = step_waves == 1 ? 256 : step_waves == 2 ? 512
@@ -3582,7 +3587,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
                                R, spb_f, rec, adjm, step_waves == 1 ? 1 : 0);
         }
-        if (timing) { (void)hipEventRecord(ev[2], st); (void)hipEventRecord(ev[3], st); }
+        if (tk2) (void)hipEventRecord(ev[2], st);
+        if (tall) (void)hipEventRecord(ev[3], st);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
@@ -3617,7 +3623,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             gbh.count = gb.count + h;
             gbh.list = gb.list + g0;
             hipEvent_t* eh = ev + 4 * h;
-            if (timing) (void)hipEventRecord(eh[0], sh);
+            if (tall) (void)hipEventRecord(eh[0], sh);
             const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
             if (prep_w4(v1 - v0, device)) {
                 if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
@@ -3626,16 +3632,16 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                 if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
                 else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             }
-            if (timing) (void)hipEventRecord(eh[1], sh);
+            if (tk2) (void)hipEventRecord(eh[1], sh);
             const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
             hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
             hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
-            if (timing) (void)hipEventRecord(eh[2], sh);
+            if (tk2) (void)hipEventRecord(eh[2], sh);
             hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
                                rec, adjm, v0, v1);
-            if (timing) (void)hipEventRecord(eh[3], sh);
+            if (tall) (void)hipEventRecord(eh[3], sh);
         }
         for (int k = 0; k < NP - 1; k++)
             if (hipEventRecord(W.join[k], W.st2[k]) != hipSuccess || hipStreamWaitEvent(st, W.join[k], 0) != hipSuccess)
@@ -3648,7 +3654,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         const int threads = 256;
         const int G = prep_group(Sv);
         const int64_t blocks = (Sv * G + threads - 1) / threads;
-        if (timing) (void)hipEventRecord(ev[0], st);
+        if (tall) (void)hipEventRecord(ev[0], st);
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
 #define PP_LAUNCH_PREP(KER) \
@@ -3677,7 +3683,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         const unsigned nb = (unsigned)cg.groups;
         const unsigned nslow = (unsigned)std::min<int64_t>(cg.groups, 2048);
         const int64_t ng = cg.groups;
-        if (timing) (void)hipEventRecord(ev[1], st);
+        if (tk2) (void)hipEventRecord(ev[1], st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
                            cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0);          \
@@ -3692,7 +3698,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         else { PP_LAUNCH_CAND(0); }
 #undef PP_LAUNCH_CAND
     }
-    if (timing) (void)hipEventRecord(ev[2], st);
+    if (tk2) (void)hipEventRecord(ev[2], st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
     if (ref_direct && !P.emit_paths && !emit_in) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
@@ -3709,7 +3715,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
         hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
     }
-    if (timing) (void)hipEventRecord(ev[3], st);
+    if (tall) (void)hipEventRecord(ev[3], st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
     return PP_OK;
 }
@@ -3743,7 +3749,7 @@ int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
     if (!M || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
     std::lock_guard<std::mutex> lk(M->mu);
     DevState& D = M->dev[device];
-    D.timing = enable != 0;
+    D.timing = enable == PP_TIMING_K2 ? 2 : (enable != 0 ? 1 : 0);
     if (D.timing) {
         // the events of 256 calls made now, outside any timed region (pp_eval takes 8 per call
         // from the pool, pp_timing_read returns them)
@@ -3770,13 +3776,16 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     const size_t ng = D.ev_rec.size() / EG;
     for (size_t i = 0; i < ng; i++) {
         const int kind = D.ev_kind[i], parts = (kind >> 1) & 7;
+        const bool k2only = (kind & 16) != 0;
         for (int h = 0; h < (parts ? parts : 1); h++) {
             hipEvent_t* e = &D.ev_rec[EG * i + 4 * h];
-            if (hipEventSynchronize(e[3]) != hipSuccess) rc = PP_ERR_HIP;
+            if (hipEventSynchronize(k2only ? e[2] : e[3]) != hipSuccess) rc = PP_ERR_HIP;
             float t;
-            if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
+            if (!k2only && !(kind & 32)) {
+                if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
+            }
             if (hipEventElapsedTime(&t, e[1], e[2]) == hipSuccess) { ms3[1] += t; launches3[1]++; } else rc = PP_ERR_HIP;
-            if (kind & 1) {
+            if ((kind & 1) && !k2only) {
                 if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
             }
         }

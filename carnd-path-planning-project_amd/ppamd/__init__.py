@@ -290,7 +290,8 @@ class Map:
         _check(lib.pp_reserve(self.handle, device, max_scenes), "pp_reserve")
 
     def timing(self, device, enable=True):
-        _check(lib.pp_timing_enable(self.handle, device, 1 if enable else 0), "pp_timing_enable")
+        """Per-kernel HIP-event timing: False off, True every kernel, TIMING_K2 K2's events only."""
+        _check(lib.pp_timing_enable(self.handle, device, int(enable)), "pp_timing_enable")
 
     def read_timing(self, device):
         """(ms per kernel [k_prep, k_cand, k_winner], launches per kernel); clears the record."""
@@ -546,6 +547,9 @@ def plan_frame(m: Map, ego_x, ego_y, ego_yaw_deg, ego_speed_mph, prev_x, prev_y,
 
 DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
 
+
+# pp_timing_enable modes (include/pp.h PP_TIMING_*)
+TIMING_ALL, TIMING_K2 = 1, 2
 
 # pp_debug_set keys and launch shapes (include/pp.h PP_DBG_*, PP_SHAPE_*)
 DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT = 0, 1, 2, 3, 4

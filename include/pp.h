@@ -401,10 +401,14 @@ int32_t pp_debug_set(int32_t key, int32_t value);
 int32_t pp_debug_get(int32_t key);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
- * (K1 k_prep, K2 k_cand, K3/K4 k_winner or k_emit; a two-stream split call (PP_DBG_SPLIT) counts
- * two launches of each, each half timed on its own stream). pp_timing_read synchronises on the
- * recorded events, returns the summed milliseconds and launch counts per kernel, and clears the
- * record. */
+ * (K1 k_prep, K2 k_cand, K3/K4 k_winner or k_emit; a split call (PP_DBG_SPLIT) counts one launch of
+ * each per part, each part timed on its own stream). enable PP_TIMING_K2 records only K2's two
+ * events per launch (an event costs a few microseconds of stream time: the bench's timed region
+ * records only what its roofline needs); any other nonzero value, every kernel's. pp_timing_read
+ * synchronises on the recorded events, returns the summed milliseconds and launch counts per kernel
+ * (k_prep and k_winner/k_emit 0 launches under PP_TIMING_K2), and clears the record. */
+#define PP_TIMING_ALL 1
+#define PP_TIMING_K2  2
 int32_t pp_timing_enable(pp_map* m, int32_t device, int32_t enable);
 int32_t pp_timing_read(pp_map* m, int32_t device, double* ms3, int64_t* launches3);
 
