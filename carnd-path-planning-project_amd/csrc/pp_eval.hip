@@ -343,11 +343,15 @@ __device__ __forceinline__ void prep_ego(const MapV& m, const pp_scene_batch& in
     e.ego_acc = 0; e.esv_x = 0; e.esv_y = 0; e.dt0 = 0;
     e.K = 0;
     e.p8x = 0; e.p8y = 0;
-    if (in.n_prev[s] >= PP_PREV_KEEP) {
+    // (the kept points are loaded with n_prev, not after it: rows 7-9 always exist, and a frame's
+    // K1 would otherwise wait for two memory round trips in a row)
+    const int np = in.n_prev[s];
+    const double p7x = in.prev_x[7 * S + s], p7y = in.prev_y[7 * S + s];
+    const double p8x = in.prev_x[8 * S + s], p8y = in.prev_y[8 * S + s];
+    const double p9x = in.prev_x[9 * S + s], p9y = in.prev_y[9 * S + s];
+    if (np >= PP_PREV_KEEP) {
         e.K = PP_PREV_KEEP;
-        const double p7x = in.prev_x[7 * S + s], p7y = in.prev_y[7 * S + s];
-        e.p8x = in.prev_x[8 * S + s]; e.p8y = in.prev_y[8 * S + s];
-        const double p9x = in.prev_x[9 * S + s], p9y = in.prev_y[9 * S + s];
+        e.p8x = p8x; e.p8y = p8y;
         const double ax = e.p8x - p7x, ay = e.p8y - p7y;
         const double v2 = sqrt(ax * ax + ay * ay);
         e.esv_x = p9x - e.p8x; e.esv_y = p9y - e.p8y;
@@ -972,6 +976,15 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
     const int T_in = in.prev_target_lane[s];
     PlanAcc a;
     a.init();
+    // row r of the first G rows, loaded with n_cars rather than after it (rows below car_stride
+    // exist; the frame's K1 waits for one memory round trip here, not two)
+    int pid0 = 0;
+    double px0 = 0, py0 = 0, pvx0 = 0, pvy0 = 0;
+    if (r < in.car_stride) {
+        const int64_t ix = (int64_t)r * S + s;
+        pid0 = in.car_id[ix];
+        px0 = in.car_x[ix]; py0 = in.car_y[ix]; pvx0 = in.car_vx[ix]; pvy0 = in.car_vy[ix];
+    }
     int ncar = in.n_cars[s];
     if (ncar > in.car_stride) ncar = in.car_stride;
     // Without a car table: the frame's rows. With one (the reference's persistent std::map, as
@@ -1012,10 +1025,11 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
                 const int pl = p0 + r;
                 int pid = 0;
                 double px = 0, py = 0, pvx = 0, pvy = 0;
-                if (pl < ncar) {
+                if (p0 == 0) {                // (the rows loaded ahead)
+                    if (pl < ncar) { pid = pid0; px = px0; py = py0; pvx = pvx0; pvy = pvy0; }
+                } else if (pl < ncar) {
                     const int64_t ix = (int64_t)pl * S + s;
                     pid = in.car_id[ix];
-                    if (ncar <= G) { px = in.car_x[ix]; py = in.car_y[ix]; pvx = in.car_vx[ix]; pvy = in.car_vy[ix]; }
                 }
                 const int nq = ncar - p0 < G ? ncar - p0 : G;
                 for (int q = 0; q < nq; q++) {
@@ -1041,6 +1055,9 @@ __device__ __forceinline__ void prep_grp_eval(const MapV& m, const pp_scene_batc
                 double cx, cy, cvx, cvy;
                 if (fgot) {                   // (tab: the row's id is the slot's)
                     cx = fx; cy = fy; cvx = fvx; cvy = fvy;
+                } else if (!tab && j0 == 0) { // row j = r: loaded ahead
+                    id = pid0;
+                    cx = px0; cy = py0; cvx = pvx0; cvy = pvy0;
                 } else {
                     id = in.car_id[ix];
                     cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
