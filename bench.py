@@ -602,8 +602,8 @@ def main(argv=None):
     # dominant kernel: k_cand on this rank
     k_cand_ms = kms["k_cand"]
     bpc = algorithmic_bytes_per_candidate(Cn, a.n_points, a.emit_paths)
-    # K2 launches per step: 2 where pp_eval splits the batch over two streams (shard sizes), each
-    # launch timed on its own stream and covering half the candidates
+    # K2 stages per step (1: pp_eval times a split batch's overlapping parts as one stage, the span
+    # from the first part's K2 start to the last part's K2 end)
     k2_per_step = max(launches[1] // max(a.steps * frames, 1), 1)
     cands_launch = S * Cn // k2_per_step
     achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
@@ -642,7 +642,8 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": k_cand_ms, "launches_per_step": k2_per_step,
-                     "kernel_time_source": "HIP events around each K2 launch on its own stream, timed region",
+                     "kernel_time_source": ("HIP events around each K2 launch on its own stream, timed region "
+                                            "(a batch split over streams: the span of its parts' K2 launches)"),
                      "frac_rocprof": (bpc * cands_launch / (rp["dominant_ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                                       if rp else None),
                      "kernel_ms_rocprof": rp["dominant_ms_per_launch"] if rp else None,

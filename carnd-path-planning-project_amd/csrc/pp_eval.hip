@@ -3791,20 +3791,32 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     int rc = PP_OK;
     constexpr int EG = 4 * kSplitMax;
     const size_t ng = D.ev_rec.size() / EG;
+    // signed milliseconds from a to b (either order)
+    auto dt = [&](hipEvent_t a, hipEvent_t b, float& t) {
+        if (hipEventElapsedTime(&t, a, b) == hipSuccess) return true;
+        if (hipEventElapsedTime(&t, b, a) == hipSuccess) { t = -t; return true; }
+        rc = PP_ERR_HIP;
+        return false;
+    };
     for (size_t i = 0; i < ng; i++) {
-        const int kind = D.ev_kind[i], parts = (kind >> 1) & 7;
+        const int kind = D.ev_kind[i], parts = (kind >> 1) & 7, np = parts ? parts : 1;
         const bool k2only = (kind & 16) != 0;
-        for (int h = 0; h < (parts ? parts : 1); h++) {
-            hipEvent_t* e = &D.ev_rec[EG * i + 4 * h];
-            if (hipEventSynchronize(k2only ? e[2] : e[3]) != hipSuccess) rc = PP_ERR_HIP;
-            float t;
-            if (!k2only && !(kind & 32)) {
-                if (hipEventElapsedTime(&t, e[0], e[1]) == hipSuccess) { ms3[0] += t; launches3[0]++; } else rc = PP_ERR_HIP;
+        hipEvent_t* e0 = &D.ev_rec[EG * i];
+        for (int h = 0; h < np; h++)
+            if (hipEventSynchronize(k2only ? e0[4 * h + 2] : e0[4 * h + 3]) != hipSuccess) rc = PP_ERR_HIP;
+        // stage k (0: K1, 1: K2, 2: K3/K4) of a call: from its earliest start to its latest end over
+        // the parts (one stream: the kernel's own interval; a split call's parts overlap, and the
+        // stage's time is the span they cover together, as in a kernel trace), one launch per call
+        for (int k = 0; k < 3; k++) {
+            if (k != 1 && (k2only || (k == 0 && (kind & 32)) || (k == 2 && !(kind & 1)))) continue;
+            float lo = 0, hi = 0;
+            bool ok = true;
+            for (int h = 0; h < np && ok; h++) {
+                float a, b;
+                ok = dt(e0[1], e0[4 * h + k], a) && dt(e0[1], e0[4 * h + k + 1], b);
+                if (ok) { lo = h == 0 ? a : std::min(lo, a); hi = h == 0 ? b : std::max(hi, b); }
             }
-            if (hipEventElapsedTime(&t, e[1], e[2]) == hipSuccess) { ms3[1] += t; launches3[1]++; } else rc = PP_ERR_HIP;
-            if ((kind & 1) && !k2only) {
-                if (hipEventElapsedTime(&t, e[2], e[3]) == hipSuccess) { ms3[2] += t; launches3[2]++; } else rc = PP_ERR_HIP;
-            }
+            if (ok) { ms3[k] += hi - lo; launches3[k]++; }
         }
         for (int k = 0; k < EG; k++) D.ev_pool.push_back(D.ev_rec[EG * i + k]);
     }

@@ -401,8 +401,9 @@ int32_t pp_debug_set(int32_t key, int32_t value);
 int32_t pp_debug_get(int32_t key);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around every kernel of pp_eval
- * (K1 k_prep, K2 k_cand, K3/K4 k_winner or k_emit; a split call (PP_DBG_SPLIT) counts one launch of
- * each per part, each part timed on its own stream). enable PP_TIMING_K2 records only K2's two
+ * (K1 k_prep, K2 k_cand, K3/K4 k_winner or k_emit; a split call (PP_DBG_SPLIT) times each part on
+ * its own stream and counts each stage once, as the span from its earliest part's start to its
+ * latest part's end: the parts overlap). enable PP_TIMING_K2 records only K2's two
  * events per launch (an event costs a few microseconds of stream time: the bench's timed region
  * records only what its roofline needs); any other nonzero value, every kernel's. pp_timing_read
  * synchronises on the recorded events, returns the summed milliseconds and launch counts per kernel

@@ -68,9 +68,9 @@ def test_workload_names():
 
 def test_rocprof_summary_entries():
     """profiles/rocprof_summary.json (tools/rocprof_summarize.py): every entry names its launch shape
-    and its K2 launches per step (2 where pp_eval splits a shard over two streams), the candidates
-    of one launch are the shape's divided by those launches, and the recomputed fraction of HBM peak
-    is the one a bench line of that shape reports as roofline.frac_rocprof."""
+    and its K2 stages per step (1: a batch split over streams is timed as the span of its parts),
+    the candidates of one stage are the shape's, and the recomputed fraction of HBM peak is the one
+    a bench line of that shape reports as roofline.frac_rocprof."""
     rp = bench.load_rocprof_all()
     assert rp, "profiles/rocprof_summary.json missing"
     for tag, e in rp.items():
@@ -83,8 +83,9 @@ def test_rocprof_summary_entries():
         bpc = bench.algorithmic_bytes_per_candidate(e["candidates_per_scene"], e["n_points"], e["emit_paths"])
         frac = bpc * e["candidates_per_launch"] / (e["dominant_ms_per_launch"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS
         assert 0 < frac < 1, tag
-    # the shard is split in two: its entry says so
-    assert rp["k_cand_S262144_C15_N50"]["launches_per_step"] == 2
+    # the shard is split in two: its entry says so, and times the two parts as one span
+    assert rp["k_cand_S262144_C15_N50"]["parts"] == 2
+    assert rp["k_cand_S262144_C15_N50"]["launches_per_step"] == 1
 
 
 def test_rocprof_summarize_tool(tmp_path):
@@ -99,11 +100,31 @@ def test_rocprof_summarize_tool(tmp_path):
             '"void k_cand<true, 1>(MapG, pp_scene_batch)",26,260000,10000.0,1,1,1,0',
             '"void k_prep<true, false>(MapG)",26,5200000,200000.0,20,1,1,0']
     (d / "run_kernel_stats.csv").write_text("\n".join(rows) + "\n")
+    # the kernel trace of 3 calls split in 2 parts: part 1 starts 0.1 ms after part 0 and each part's
+    # k_cand<false> runs 1 ms, k_cand<true> 0.01 ms after it -> 1.11 ms per call; the first call is
+    # slow (3 ms) and the median skips it
+    tr = ['"Kernel_Name","Start_Timestamp","End_Timestamp"']
+    for c, t0 in enumerate((0, 10_000_000, 20_000_000)):
+        stretch = 3 if c == 0 else 1
+        for h in range(2):
+            a = t0 + h * 100_000 * stretch
+            tr.append(f'"void k_cand<false, 1>(MapG, pp_scene_batch)",{a},{a + 1_000_000 * stretch}')
+            tr.append(f'"void k_cand<true, 1>(MapG, pp_scene_batch)",{a + 1_000_000 * stretch},{a + 1_010_000 * stretch}')
+        tr.append(f'"void k_prep<true, false>(MapG)",{t0 - 300_000},{t0 - 100_000}')
+    (d / "run_kernel_trace.csv").write_text("\n".join(tr) + "\n")
     (tmp_path / "profiles").mkdir()
-    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "rocprof_summarize.py"), str(tmp_path / "stats"),
-                        "k_cand_S262144_C15_N50", "2"], cwd=tmp_path, capture_output=True, text=True)
+    tool = os.path.join(REPO, "tools", "rocprof_summarize.py")
+    r = subprocess.run([sys.executable, tool, str(tmp_path / "stats"), "k_cand_S4096_C15_N50"],
+                       cwd=tmp_path, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    out = json.load(open(tmp_path / "profiles" / "rocprof_summary.json"))["k_cand_S262144_C15_N50"]
-    assert out["dominant_ms_per_launch"] == pytest.approx(1.01)
-    assert out["launches_per_step"] == 2 and out["candidates_per_launch"] == 262144 * 15 // 2
+    r = subprocess.run([sys.executable, tool, str(tmp_path / "stats"), "k_cand_S262144_C15_N50", "2"],
+                       cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    summary = json.load(open(tmp_path / "profiles" / "rocprof_summary.json"))
+    one = summary["k_cand_S4096_C15_N50"]
+    assert one["dominant_ms_per_launch"] == pytest.approx(1.01) and one["parts"] == 1
+    out = summary["k_cand_S262144_C15_N50"]
+    assert out["dominant_ms_per_launch"] == pytest.approx(1.11)
+    assert out["launches_per_step"] == 1 and out["parts"] == 2 and out["dominant_launches"] == 3
+    assert out["candidates_per_launch"] == 262144 * 15
     assert "k_prep<true, false>" in out["kernels"]

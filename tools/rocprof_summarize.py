@@ -2,11 +2,13 @@
 (read by bench.py for roofline.frac_rocprof: the same roofline fraction from the profiler's average
 kernel duration instead of the bench's own HIP events).
 
-  python3 tools/rocprof_summarize.py <dir with *kernel_stats.csv> <tag> [launches_per_step]
+  python3 tools/rocprof_summarize.py <dir with *kernel_stats.csv> <tag> [parts]
 
 <tag> is bench.py's launch-shape tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>];
-launches_per_step is the number of K2 launches per pp_eval call (2 where pp_eval splits a
-shard-sized batch over two streams, include/pp.h PP_DBG_SPLIT)."""
+parts is the number of streams pp_eval splits the batch over (include/pp.h PP_DBG_SPLIT): their K2
+launches overlap, so the K2 time of a call is the span from the first of its k_cand dispatches'
+start to the last one's end, read from the kernel trace (run_kernel_trace.csv), as pp_timing_read
+reports it; parts = 1 takes the profiler's per-dispatch averages."""
 import csv
 import glob
 import json
@@ -18,7 +20,7 @@ from shape_tags import DOMINANT, parse_tag
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    per_step = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    parts = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     files = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)
     if not files:
         raise SystemExit(f"rocprof_summarize: no *kernel_stats.csv under {src}")
@@ -34,12 +36,31 @@ def main():
     # one K2 launch = one dispatch of each dominant instantiation (k_cand<false>, k_cand<true>)
     calls = max(v["calls"] for v in dom.values())
     dom_ms = sum(v["total_ms"] for v in dom.values()) / calls
+    how = "per-dispatch averages"
+    if parts > 1:
+        # the dominant dispatches in launch order, 2 per part (k_cand<false>, k_cand<true>) per call
+        tr = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
+        if not tr:
+            raise SystemExit(f"rocprof_summarize: parts > 1 needs the kernel trace under {src}")
+        rows = [r for r in csv.DictReader(open(tr[0]))
+                if r["Kernel_Name"].split("(")[0].replace("void ", "").strip().startswith(DOMINANT)]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        per = 2 * parts
+        spans = []
+        for c0 in range(0, len(rows) - per + 1, per):
+            grp = rows[c0:c0 + per]
+            spans.append((max(int(r["End_Timestamp"]) for r in grp) - min(int(r["Start_Timestamp"]) for r in grp)) * 1e-6)
+        if not spans:
+            raise SystemExit("rocprof_summarize: no complete call in the kernel trace")
+        # the median call: the first call's parts load the code object one after the other
+        dom_ms = sorted(spans)[len(spans) // 2]
+        calls = len(spans)
+        how = f"median span of a call's {per} k_cand dispatches ({parts} overlapping parts), kernel trace"
     shape = parse_tag(tag)
-    shape["candidates_per_launch"] //= per_step
     p = "profiles/rocprof_summary.json"
     out = json.load(open(p)) if os.path.exists(p) else {}
-    out[tag] = dict(shape, **{"launches_per_step": per_step, "dominant_ms_per_launch": dom_ms,
-                              "dominant_launches": calls, "kernels": kernels,
+    out[tag] = dict(shape, **{"launches_per_step": 1, "parts": parts, "dominant_ms_per_launch": dom_ms,
+                              "dominant_launches": calls, "dominant_time": how, "kernels": kernels,
                               "source": f"rocprofv3 --kernel-trace --stats of bench.py ({src}, summarised into profiles/)"})
     json.dump(out, open(p, "w"), indent=1, sort_keys=True)
     print("wrote", p, tag, f"dominant {dom_ms:.4f} ms per launch")
