@@ -3102,8 +3102,11 @@ bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // Two-stream split (reference mode, no paths): batches of about one 8-GPU shard of BASELINE config 5
 // (262,144 scenes) run as two halves, each K1 -> K2 -> K4 on its own stream, so one half's kernels
 // fill the other's start-up and tail (a batch this size is ~15 rounds of k_cand blocks and one of
-// k_prep waves). PP_DBG_SPLIT 1 forces it (any split-eligible batch), 2 off.
-constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 786432;
+// k_prep waves). Up to config 5's N = 2 shard (1,048,576 scenes: 4.96-4.99 ms against
+// 5.09-5.15 unsplit, same boxes); the full 2,097,152-scene batch stays one stream (9.87-9.91 against
+// 9.93-9.96 ms split, within the boxes' spread, and its K2 span is 0.3 ms longer than the unsplit
+// K2). PP_DBG_SPLIT 1 forces it (any split-eligible batch), 2 off.
+constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 1572864;
 bool split_on(int64_t S) {
     const int f = dbg(PP_DBG_SPLIT);
     if (f == 2) return false;
@@ -3616,8 +3619,9 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         // split_parts(S) parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
         // their scenes, part 0 on the caller's stream, part h > 0 on stream st2[h - 1]; each part
         // its own flagged-group list (count word h, its list from its first group's index on).
-        // Timing: each part's kernels by events on its own stream (P launches of each kernel per
-        // call; they overlap the other parts', as in a rocprofv3 kernel trace of the same call).
+        // Timing: each part's kernels by events on its own stream; pp_timing_read counts each stage
+        // once per call, the span from the first part's start to the last part's end (the parts
+        // overlap, so one part's duration understates the stage's throughput).
         const int NP = split_parts(S);
         if (!W.fork && hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
         for (int k = 0; k < NP - 1; k++)

@@ -384,9 +384,9 @@ int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
  *                      winner record, staging copies, new car-table slots) and checks that the
  *                      slow-group bitmap is all zero (PP_ERR_STATE otherwise), so no kernel can pass
  *                      a test on what an earlier call left behind
- *   PP_DBG_SPLIT       two-stream split of reference-mode batches (two halves, each K1 -> K2 -> K4
- *                      on its own stream): 1 on wherever possible, 2 off (0: batches of 131,072 to
- *                      786,432 scenes)
+ *   PP_DBG_SPLIT       multi-stream split of reference-mode batches (2 or 3 parts, each K1 -> K2 ->
+ *                      K4 on its own stream): 1 on wherever possible, 2 off (0: batches of 131,072
+ *                      to 1,572,864 scenes)
  * Returns PP_ERR_ARG for an unknown key or value. */
 #define PP_DBG_PREP_GROUP  0
 #define PP_DBG_PREP_WAVES  1

@@ -1,5 +1,5 @@
 """The multi-stream split (pp_eval, include/pp.h PP_DBG_SPLIT): reference-mode batches of about a
-4- or 8-GPU shard's size run as 2 parts (up to 393,216 scenes) or 3 parts, each K1 -> K2 -> K4 on
+2-, 4- or 8-GPU shard's size run as 2 parts (up to 393,216 scenes) or 3 parts, each K1 -> K2 -> K4 on
 its own stream. The parts write disjoint ranges of every buffer and keep separate flagged-group
 lists, so the results must be the one-stream launch's BIT FOR BIT, including the scenes routed to
 k_cand<true> and part boundaries that split no group; a sample is checked against the oracle."""
@@ -31,7 +31,8 @@ def run(env, sc, prm, mode):
     return ppamd.result_to_numpy(r)
 
 
-@pytest.mark.parametrize("S,mode", [(140000, ppamd.SPLIT_AUTO), (420000, ppamd.SPLIT_AUTO), (20000, ppamd.SPLIT_ON),
+@pytest.mark.parametrize("S,mode", [(140000, ppamd.SPLIT_AUTO), (420000, ppamd.SPLIT_AUTO), (1048583, ppamd.SPLIT_AUTO),
+                                    (20000, ppamd.SPLIT_ON),
                                     (20011, ppamd.SPLIT_ON)])
 def test_split_bit_identical(env, S, mode):
     sc = ppamd.synth_host(env["m"], S, seed=S, first=S)
