@@ -15,11 +15,15 @@ rp() { name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --stats --outp
 rp stats5
 rp stats3 --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
 rp stats_shard --scenes 262144
+rp stats_524288 --scenes 524288
+rp stats_1048576 --scenes 1048576
 rp stats4 --draws 64 --n-speeds 1 --scenes 16384
 rp stats2 --scenes 4096 --steps 300 --warmup 30
 python3 tools/rocprof_summarize.py $OUT/stats5 k_cand_S2097152_C15_N50 1
 python3 tools/rocprof_summarize.py $OUT/stats3 k_cand_S262144_C24_N100_paths 1
 python3 tools/rocprof_summarize.py $OUT/stats_shard k_cand_S262144_C15_N50 2
+python3 tools/rocprof_summarize.py $OUT/stats_524288 k_cand_S524288_C15_N50 3
+python3 tools/rocprof_summarize.py $OUT/stats_1048576 k_cand_S1048576_C15_N50 3
 python3 tools/rocprof_summarize.py $OUT/stats4 k_cand_S16384_C192_N50_D64 1
 python3 tools/rocprof_summarize.py $OUT/stats2 k_cand_S4096_C15_N50 1
 cp profiles/rocprof_summary.json $OUT/rocprof_summary.json
