@@ -14,6 +14,7 @@
 //                (reference mode: the winner is known before the loop; k_cand's first wave of
 //                each block runs the winners and writes next_x/next_y)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
@@ -3592,22 +3593,25 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     if (step_fused) {
         if (timing) DS.ev_kind.back() |= 32;          // (no K1 kernel: K1 runs inside the step)
         if (tall) (void)hipEventRecord(ev[0], st);
-        if (tk2) (void)hipEventRecord(ev[1], st);
         // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
         const int threads_f = step_waves == 1 ? 256 : step_waves == 2 ? 512
                                                       : std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
+        // the step kernel's own start/end timestamps go into K2's events (the launch's dispatch
+        // records them): no marker packets in the stream, which cost a few us each in a ~0.1 ms step
+        hipEvent_t e1 = tk2 ? ev[1] : nullptr, e2 = tk2 ? ev[2] : nullptr;
         if (fio) {
+            if (tk2) (void)hipEventRecord(ev[1], st);
             hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, *fio, mg, B, P, pv, R, spb_f,
                                rec, adjm, step_waves == 1 ? 1 : 0);
+            if (tk2) (void)hipEventRecord(ev[2], st);
         } else if (step_waves == 2) {
-            hipLaunchKernelGGL(k_step_small512, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P,
-                               pv, R, spb_f, rec, adjm);
+            hipExtLaunchKernelGGL(k_step_small512, dim3((unsigned)groups_f), dim3(threads_f), (uint32_t)lds_f, st,
+                                  e1, e2, 0u, mg, B, P, pv, R, spb_f, rec, adjm);
         } else {
-            hipLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), lds_f, st, mg, B, P, pv,
-                               R, spb_f, rec, adjm, step_waves == 1 ? 1 : 0);
+            hipExtLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), (uint32_t)lds_f, st,
+                                  e1, e2, 0u, mg, B, P, pv, R, spb_f, rec, adjm, step_waves == 1 ? 1 : 0);
         }
-        if (tk2) (void)hipEventRecord(ev[2], st);
         if (tall) (void)hipEventRecord(ev[3], st);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
