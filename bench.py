@@ -118,6 +118,30 @@ def load_rocprof_all():
         return {}
 
 
+def stamped(entry, sha):
+    """A profile summary entry (pmc_summary.json / rocprof_summary.json) applies to this run only if
+    it was measured on the same library build: its lib_sha256 equals the loaded library's."""
+    return bool(entry) and entry.get("lib_sha256") == sha
+
+
+def profile_entries(pmc, rp, sha):
+    """(pmc, rp, stamp): the PMC and kernel-trace entries of this launch shape kept only when their
+    library stamp matches the loaded library (else None: their counts describe another binary), and
+    a record of which were dropped."""
+    stamp = {"lib_sha256": sha,
+             "pmc": None if not pmc else ("match" if stamped(pmc, sha) else "stale: " + str(pmc.get("lib_sha256"))),
+             "rocprof": None if not rp else ("match" if stamped(rp, sha) else "stale: " + str(rp.get("lib_sha256")))}
+    return (pmc if stamped(pmc, sha) else None), (rp if stamped(rp, sha) else None), stamp
+
+
+def shard_projection(t_full, t_shards):
+    """Projected strong-scaling speed-ups of config 5 from same-process shard timings: N GPUs each
+    evaluate one 1/N shard (no collective), so the job takes the shard's time and the speed-up over
+    one GPU is t(full batch) / t(shard of N)."""
+    return {str(n): {"speedup": t_full / t, "efficiency": t_full / t / n, "shard_ms_per_step": t * 1e3}
+            for n, t in sorted(t_shards.items())}
+
+
 def pmc_tag(S, Cn, N, emit_paths, D):
     return f"k_cand_S{S}_C{Cn}_N{N}" + ("_paths" if emit_paths else "") + (f"_D{D}" if D > 1 else "")
 
@@ -207,6 +231,8 @@ def parse(argv=None):
     ap.add_argument("--debug", action="append", default=[], metavar="KEY=VALUE",
                     help="library debug switch for A/B runs (include/pp.h PP_DBG_*): prep_group=G, "
                          "prep_waves=3|4, shape=1|2|3; recorded in config.debug, which marks the line not reportable")
+    ap.add_argument("--no-shard-projection", action="store_true",
+                    help="skip timing config 5's 2-, 4- and 8-GPU shards after the headline (1 GPU, config 5)")
     ap.add_argument("--cpu-ranks", action="store_true",
                     help="launcher rehearsal without a GPU: every rank evaluates its shard with the CPU oracle")
     return ap.parse_args(argv)
@@ -608,11 +634,15 @@ def main(argv=None):
     cands_launch = S * Cn // k2_per_step
     achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
     pmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D)
-    traffic, traffic_pipe = roofline_fields(pmc, cands_launch, bpc, k_cand_ms)
     # the same fraction from the profiler's average K2 duration of this exact launch shape (a
     # committed rocprofv3 run of this command; durations do not carry over between batch sizes)
     rp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D))
     rp = rp if rp and rp.get("launches_per_step") == k2_per_step and not a.rollout else None
+    # counters and profiler durations of another library build describe another binary: dropped
+    pmc, rp, stamp = profile_entries(pmc, rp, ppamd.lib_sha256())
+    traffic, traffic_pipe = roofline_fields(pmc, cands_launch, bpc, k_cand_ms)
+    # the small-batch shapes run the whole step in one launch: its events time K1 + K2 + K4
+    fused_step = bool(launches_all[1]) and not launches_all[0] and not a.rollout
     wname = workload_name(S, Cn, a.n_speeds, a.n_points, a.emit_paths, D, a.rollout)
     out = {
         "metric": "candidate trajectories/sec (spline+cost, 50-pt horizon) at 1/2/4/8 MI355X",
@@ -642,8 +672,11 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel_ms": k_cand_ms, "launches_per_step": k2_per_step,
-                     "kernel_time_source": ("HIP events around each K2 launch on its own stream, timed region "
+                     "kernel_time_source": ("the whole one-launch step (K1 + K2 + K4 in one kernel: its "
+                                            "dispatch's own start/end events), timed region" if fused_step else
+                                            "HIP events around each K2 launch on its own stream, timed region "
                                             "(a batch split over streams: the span of its parts' K2 launches)"),
+                     "profile_stamp": stamp,
                      "frac_rocprof": (bpc * cands_launch / (rp["dominant_ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                                       if rp else None),
                      "kernel_ms_rocprof": rp["dominant_ms_per_launch"] if rp else None,
@@ -681,6 +714,17 @@ def main(argv=None):
                                           "tools/valu_peak.hip"}
     if a.rollout:
         out["scene_frames_per_s"] = total_scenes * a.steps * frames / elapsed
+    if (world == 1 and a.scaling == "strong" and wname == "BASELINE config 5" and S == CONFIG5_SCENES
+            and not a.debug and not a.no_shard_projection):
+        # the 2-, 4- and 8-GPU shards of the same batch, timed in this process on this GPU right
+        # after the headline (same box, same build): the projected N-GPU speed-ups
+        t_sh = {}
+        for n in (2, 4, 8):
+            el_n, _, _ = measure(0, CONFIG5_SCENES // n, a.steps, a.warmup)
+            t_sh[n] = el_n / a.steps
+        out["shard_projection"] = dict(shard_projection(elapsed / a.steps, t_sh), what=(
+            "config 5 on N GPUs = N independent shards of 2,097,152 / N scenes (no collective): speed-up "
+            "t(full batch) / t(shard), both timed in this run (same protocol, steps and warmup)"))
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
         model, nproc, share = host_cpu()
         threads = a.cpu_threads or share

@@ -46,6 +46,14 @@ __device__ __forceinline__ void diag(int k, bool c) {
 #else
 #define PP_DIAGC(k, c) ((void)0)
 #endif
+#ifdef PP_CENSUS
+// census builds only (-DPP_CENSUS): an assembly comment ";@R <output mode> <region>" at the start of
+// each region of the candidate loop; tools/valu_census.py counts each region's instructions in the
+// build's ISA and multiplies them by how often a wave executes the region (tools/diag_events.py)
+#define PP_REGION(name) asm volatile(";@R %0 " name ::"i"(kOutMode))
+#else
+#define PP_REGION(name) ((void)0)
+#endif
 #ifdef PP_CHECK
 // checking builds only (-DPP_CHECK): every global store of k_cand / k_emit (and the record reads
 // of k_emit) is tested against the buffer it belongs to, and k_cand poisons its LDS slots at the
@@ -240,6 +248,67 @@ __device__ __forceinline__ double turn_angle_fast(double nc, double speed, doubl
     if (adiff < 0) nad = -nad;
     return nad - adiff;
 }
+// Round 5 (PP_PATHS_INC, default on): k_cand's all-paths frame without a centre. The reference's
+// turn rotates the centre about the current output point tp (src/main.cpp:995-1004), so tp stays
+// where it is and every later point is o_{k+1} = o_k + R_{k+1} (p_{k+1} - p_k): the loop keeps the
+// last output point o and the heading (ca, sa) only, and a point is o plus the rotated local step
+// (frame_step: the same four fused multiply-adds as frame_pt_fma). A narrow turn (the step's
+// angle came from asin(u_prev x u): |adiff| <= 0.0709) rotates by rot = nad - adiff, i.e. by
+// R(nad) R(-adiff), and (cos, sin)(adiff) are the step's own unit-vector products (dt, cr): only
+// sin/cos of |nad| < |adiff| are left, short Taylor polynomials (sincos_small). The points differ
+// from the reference's by rounding only (the summed steps: ~1e-13 m over a 100-point path); no
+// decision reads them.
+#ifndef PP_PATHS_INC
+#define PP_PATHS_INC 1
+#endif
+#ifndef PP_RCP1
+#define PP_RCP1 0
+#endif
+#ifndef PP_DT_NARROW
+#define PP_DT_NARROW 0
+#endif
+
+// a narrow step turn (asin_small's domain): u_prev . u > 0 and |u_prev x u| <= kStepSinMax; for unit
+// vectors (to a few ulps) the same as u_prev . u >= sqrt(1 - kStepSinMax^2) (PP_DT_NARROW: one
+// compare; |cr| then exceeds kStepSinMax by < 1e-14 at most, where the series is as accurate)
+#if PP_DT_NARROW
+#define PP_NARROW(dt, cr) ((dt) >= 0.99749053128338025)
+#else
+#define PP_NARROW(dt, cr) ((dt) > 0 && fabs(cr) <= ppm::kStepSinMax)
+#endif
+__device__ __forceinline__ void frame_step(double ca, double sa, double dpx, double dpy, double& ox, double& oy) {
+    ox = __builtin_fma(dpx, ca, __builtin_fma(-dpy, sa, ox));
+    oy = __builtin_fma(dpx, sa, __builtin_fma(dpy, ca, oy));
+}
+// sin and cos of |x| <= 0.0709: sin through x^7 (next term x^9/9! < 1.3e-16), cos through x^8 (next
+// term x^10/10! < 1e-18)
+__device__ __forceinline__ void sincos_small(double x, double& s, double& c) {
+    const double z = x * x;
+    double ps = __builtin_fma(z, kc(-1.98412698412698412698e-04), kc(8.33333333333333333333e-03));
+    ps = __builtin_fma(z, ps, kc(-1.66666666666666666667e-01));
+    s = __builtin_fma(x * z, ps, x);
+    double pc = __builtin_fma(z, kc(2.48015873015873015873e-05), kc(-1.38888888888888888889e-03));
+    pc = __builtin_fma(z, pc, kc(4.16666666666666666667e-02));
+    pc = __builtin_fma(z, pc, -0.5);
+    c = __builtin_fma(z, pc, 1.0);
+}
+// the heading turned by (cr, sr) = (cos, sin) of the rotation
+__device__ __forceinline__ void frame_rot(double& ca, double& sa, double cr, double sr) {
+    const double nca = __builtin_fma(ca, cr, -(sa * sr)), nsa = __builtin_fma(sa, cr, ca * sr);
+    ca = nca;
+    sa = nsa;
+}
+// a narrow turn: nad = +-nc / speed / 50 with adiff's sign (src/main.cpp:983-984; adiff is never
+// -0: x - pi rounds an exact cancellation to +0), (cos, sin)(rot) = R(nad) applied to (dt, -cr)
+__device__ __forceinline__ void turn_narrow(double& ca, double& sa, double nc, double speed, double adiff,
+                                            double dt, double cr) {
+    double r = __builtin_amdgcn_rcp(speed);
+    r = __builtin_fma(__builtin_fma(-speed, r, 1.0), r, r);
+    const double nad = __builtin_copysign((nc * 0.02) * r, adiff);
+    double sn, cn;
+    sincos_small(nad, sn, cn);
+    frame_rot(ca, sa, __builtin_fma(cn, dt, sn * cr), __builtin_fma(sn, dt, -(cn * cr)));
+}
 // Tuning constants (each measured against its alternatives):
 #ifndef PP_EMIT_CHUNK
 #define PP_EMIT_CHUNK 4
@@ -248,7 +317,10 @@ constexpr int kEmitChunk = PP_EMIT_CHUNK;   // emit_scene_pre (small batches): r
 constexpr int kEmitRows = 8;       // k_emit (large batches, emit_scene_rows): output rows per load round
 constexpr int kWalkPf = 4;         // segments of the control-point walk loaded ahead (get_lane_pos_fwd)
 constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
-constexpr int kCandWaves = 4;      // k_cand waves per SIMD (<= 128 VGPRs)
+#ifndef PP_CAND_WAVES
+#define PP_CAND_WAVES 4
+#endif
+constexpr int kCandWaves = PP_CAND_WAVES;   // k_cand waves per SIMD (<= 128 VGPRs)
 // Winner record (k_cand -> k_emit), room = N - K steps of scene s, rstride = room S: point-major
 // arrays, pos_x at rec[g S + s], pos_y at rec[rstride + g S + s], the rotation of an adjusted step
 // at rec[2 rstride + g S + s] (every address of scene s is = s mod S: a wave's accesses coalesce)
@@ -1536,11 +1608,19 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     double arg = 0, prev_speed = sc.start;
     double uxp = 1.0, uyp = 0.0;     // previous step direction (angle 0: the local frame's x axis)
     // 1 / (target - start) for SpeedController::override_speed (constant over the walk)
+#if PP_RCP1
+    // (both reciprocals feed only Markstein-corrected quotients: ppm::rcp_nr1 is enough)
+    const double rds = ppm::rcp_nr1(sc.target - sc.start);
+    double rtt = ppm::rcp_nr1(sc.ttime);
+#else
     const double rds = ppm::rcp_nr(sc.target - sc.start);
     double rtt = ppm::rcp_nr(sc.ttime);
+#endif
+    PP_DIAGC(20, true);     // (waves entering the loop)
     // the divisions by 50 and by the ramp time: reciprocal + correction (k_cand<false>: unchecked)
 #define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div50_nc(v))
     while (arg < 50 && ng < room) {
+        PP_REGION("head");
         PP_DIAGC(0, true);
         PP_DIAGC(2, !(s_max(cur_t - sc.shift, 0.0) > sc.ttime));
         double speed = sc_get_speed_r<kLarge>(sc, cur_t, rtt);
@@ -1548,6 +1628,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         const double x = arg + dstep;
         // tk::spline::operator() (spline.h:375-396)
         if (!(seg_lo < x && x <= seg_hi)) {
+            PP_REGION("seg");
             // forward miss (x passed the cached segment's end; the first step starts from cnt = -1,
             // seg_hi = -inf): x(cnt) = seg_hi < x is known, so the walk resumes one knot further
             // and the bounds come from the walk's own reads — one LDS round trip for the knot and
@@ -1567,6 +1648,8 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 sx = cnt > 0 ? xlo : xhi;
                 sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
             } else {
+                PP_REGION("segback");
+                PP_DIAGC(21, true);
                 if (cnt < 0) cnt = 0;
                 while (cnt < nk && sl.x(cnt) < x) cnt++;
                 while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
@@ -1577,6 +1660,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             }
             PP_DIAGC(1, true);
         }
+        PP_REGION("eval");
         const double h = x - sx;
         // the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0 (0 h + b = b, and
         // at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the last knot, whose a is
@@ -1589,9 +1673,12 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
         double ux, uy;
         {
+            PP_REGION("dir");
             const double ddx = x - pos_x, ddy = y - pos_y;
             ux = ddx * rd; uy = ddy * rd;
+            PP_DIAGC(18, !dok);
             if (__builtin_expect(!dok, 0)) {        // d == 0 implies !dok (q = 0 < 2^-900)
+                PP_REGION("dirfix");
                 if (d == 0) { ux = 1.0; uy = 0.0; }
                 // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only
                 // in k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
@@ -1605,18 +1692,23 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 }
             }
         }
+        PP_REGION("cross");
         const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
         // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
         // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
         double adiff;
-        PP_DIAGC(3, !((dt > 0 && fabs(cr) <= ppm::kStepSinMax) || speed == 0));
-        PP_DIAGC(8, ng == 0 && !(dt > 0 && fabs(cr) <= ppm::kStepSinMax));
+        PP_DIAGC(3, !((PP_NARROW(dt, cr)) || speed == 0));
+        PP_DIAGC(8, ng == 0 && !(PP_NARROW(dt, cr)));
         PP_DIAGC(9, !(dt > 0));
-        if (__builtin_expect(dt > 0 && fabs(cr) <= ppm::kStepSinMax, 1))
+        if (__builtin_expect(PP_NARROW(dt, cr), 1)) {
+            PP_REGION("asin");
             adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
-        else
+        } else {
+            PP_REGION("wide");
             // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
             adiff = ppm::fmod_2pi_small(ppm::atan2_unit(cr, dt) + 3 * kPi) - kPi;
+        }
+        PP_REGION("acc");
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
         PP_DIAGC(4, acc + cacc > P.maximum_acc);
@@ -1624,7 +1716,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
         PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
         if (acc + cacc > P.maximum_acc) {
+            PP_REGION("lim");
             if (speed > prev_speed) {                                   // :945-971
+                PP_REGION("ovr");
                 // (inside this block acc + cacc > max held: neither is NaN; k_cand<false>'s
                 // operands are finite, so the clamp is v_max_f64)
                 double na = P.maximum_acc - cacc;
@@ -1633,13 +1727,15 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 sc_override_r<kLarge>(sc, cur_t, ns, rds);
                 speed = ns;
                 sc.ttime += 0.02;
-                rtt = ppm::rcp_nr(sc.ttime);
+                rtt = PP_RCP1 ? ppm::rcp_nr1(sc.ttime) : ppm::rcp_nr(sc.ttime);
                 dstep = PP_DIV50(speed);
                 acc = na;
                 R.flags |= PP_ST_ACC_OVERRIDE;
             }
             PP_DIAGC(6, acc + cacc > P.maximum_acc);
+            PP_REGION("lim2");
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
+                PP_REGION("adj");
                 double nc = P.maximum_acc - acc;
                 if (kLarge) { if (nc < 0) nc = 0; } else nc = __builtin_fmax(nc, 0.0);
                 if (kOutMode == 2) {
@@ -1648,9 +1744,24 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                     turn_sincos<kLarge>(turn_angle<kLarge>(nc, speed, adiff), sr, cr);
                     frame_turn(F, pos_x, pos_y, cr, sr);
                 } else if (kOutMode == 4) {
+#if PP_PATHS_INC
+                    PP_DIAGC(19, !(!kLarge && PP_NARROW(dt, cr)));
+                    PP_DIAGC(23, !kLarge && PP_NARROW(dt, cr));
+                    if (!kLarge && PP_NARROW(dt, cr)) {
+                        PP_REGION("adjn");
+                        turn_narrow(F.ca, F.sa, nc, speed, adiff, dt, cr);
+                    } else {
+                        PP_REGION("adjwide");
+                        double crr, srr;
+                        turn_sincos<kLarge>(kLarge ? turn_angle<true>(nc, speed, adiff)
+                                                   : turn_angle_fast(nc, speed, adiff), srr, crr);
+                        frame_rot(F.ca, F.sa, crr, srr);
+                    }
+#else
                     double cr, sr;
                     turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), sr, cr);
                     frame_turn_at(F, pos_x, pos_y, opx, opy, cr, sr);
+#endif
                 }
                 if (kOutMode == 3 && kRec) {
                     // the turn angle for k_emit's replay of the output frame
@@ -1664,6 +1775,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 R.flags |= PP_ST_CURV_ADJUST;
             }
         }
+        PP_REGION("tail");
         cur_t += 0.02;
         prev_speed = speed;
         uxp = ux; uyp = uy;
@@ -1676,25 +1788,35 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
             const double qx = nx * rd, qy = ny * rd;
             sp_step = __builtin_fma(__builtin_fma(-qx, d, nx), rd, qx);
             dpy = __builtin_fma(__builtin_fma(-qy, d, ny), rd, qy);
-            if (__builtin_expect(!dok, 0)) { sp_step = nx / d; dpy = ny / d; }
+            if (__builtin_expect(!dok, 0)) { PP_REGION("tailfix"); sp_step = nx / d; dpy = ny / d; }
         }
+        PP_REGION("tail2");
         pos_y += dpy;
         arg += sp_step;
         pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
         if (kOutMode != 0 && kOut) {
+            PP_REGION("out");
+            PP_DIAGC(22, wx != nullptr);
             double ox, oy;
+#if PP_PATHS_INC
+            if (kOutMode == 4) { ox = opx; oy = opy; frame_step(F.ca, F.sa, sp_step, dpy, ox, oy); }
+#else
             if (kOutMode == 4) frame_pt_fma(F, pos_x, pos_y, ox, oy);
+#endif
             else frame_pt(F, pos_x, pos_y, ox, oy);
-            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { wx[ng * ws] = ox; wy[ng * ws] = oy; }
+            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { PP_REGION("outw"); wx[ng * ws] = ox; wy[ng * ws] = oy; }
+            PP_REGION("out2");
             if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                 st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
             if (kOutMode == 4) { opx = ox; opy = oy; }
         }
         if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
+        PP_REGION("latch");
         ng++;
         R.acc_sum += acc + eff_c;
         R.travelled += dstep;
     }
+    PP_REGION("end");
     R.ng = ng;
     return R;
 }
@@ -1952,9 +2074,15 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 st_xy(p0 + i * ps, in.prev_x[(int64_t)i * S + s], in.prev_y[(int64_t)i * S + s]);
             }
             double* px = p0 + K * ps;
+#ifdef PP_DIAG_NOB
+            // diagnostic builds only: phase B skipped (wrong results; measures everything else)
+            R = CandRes{0, 0, N - K, 0, 0, 0};
+            (void)sc; (void)wx; (void)wy;
+#else
             R = run_candidate<kSlow, 4>(P, sl, pv.pos_x[v], pv.pos_y[v], pv.angle[v],
                                                        pv.ca_p[v], pv.sa_p[v], sc, N - K, wx, wy, S,
                                                        px, ps);
+#endif
             for (int i = R.ng; i < N - K; i++) {
                 if (!PP_CHKP(px + i * ps + 1, paths, npaths, 8)) break;
                 st_xy(px + i * ps, __builtin_nan(""), __builtin_nan(""));
@@ -3106,12 +3234,14 @@ bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // k_prep waves). Up to config 5's N = 2 shard (1,048,576 scenes: 4.96-4.99 ms against
 // 5.09-5.15 unsplit, same boxes); the full 2,097,152-scene batch stays one stream (9.87-9.91 against
 // 9.93-9.96 ms split, within the boxes' spread, and its K2 span is 0.3 ms longer than the unsplit
-// K2). PP_DBG_SPLIT 1 forces it (any split-eligible batch), 2 off.
+// K2). PP_DBG_SPLIT 1 forces it for every batch the split can take (reference mode without paths
+// or draws, one K1 lane per scene: more than 65,536 scenes, prep_group), 2 turns it off; the parts
+// of the last call are read back with PP_DBG_LAST_PARTS.
 constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 1572864;
 bool split_on(int64_t S) {
     const int f = dbg(PP_DBG_SPLIT);
     if (f == 2) return false;
-    return f == 1 ? S >= 2048 : (S >= kSplitMin && S <= kSplitMaxScenes);
+    return f == 1 ? true : (S >= kSplitMin && S <= kSplitMaxScenes);
 }
 // parts of a split batch: 2 up to 393,216 scenes (BASELINE config 5's N = 8 shard, 262,144: 1.32 ms
 // against 1.35 / 1.37 ms with 3 / 4 parts), 3 beyond (its N = 4 shard, 524,288: 2.52 ms against
@@ -3553,22 +3683,24 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.buf = DS.map;
     mg.n = M->n;
     mg.fastm = M->fastm;
-    hipEvent_t ev[4 * kSplitMax] = {};
-    // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two)
+    // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two).
+    // The call's record is a group of 4 kSplitMax slots (before K1, after K1, after K2, after
+    // K3/K4, per part); a slot takes an event from the pool when it is first recorded, so a
+    // K2-only call takes 2 events (2 per part when split) and an all-kernel call 4 per part
     const bool timing = DS.timing != 0, tall = DS.timing == 1, tk2 = timing;
+    const size_t ev_base = DS.ev_rec.size();
     if (timing) {
-        for (int i = 0; i < 4 * kSplitMax; i++) {
-            if (DS.ev_pool.empty()) {
-                hipEvent_t e;
-                if (hipEventCreate(&e) != hipSuccess) return PP_ERR_HIP;
-                DS.ev_pool.push_back(e);
-            }
-            ev[i] = DS.ev_pool.back();
-            DS.ev_pool.pop_back();
-            DS.ev_rec.push_back(ev[i]);
-        }
+        DS.ev_rec.resize(ev_base + 4 * kSplitMax, nullptr);
         DS.ev_kind.push_back((!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0) | (tall ? 0 : 16));
     }
+    auto ev = [&](int i) -> hipEvent_t {
+        hipEvent_t& e = DS.ev_rec[ev_base + i];
+        if (!e) {
+            if (DS.ev_pool.empty() && hipEventCreate(&e) != hipSuccess) return nullptr;
+            if (!e) { e = DS.ev_pool.back(); DS.ev_pool.pop_back(); }
+        }
+        return e;
+    };
     pp_params P = *prm;
     pp_scene_batch B = *in;
     pp_result R = *out;
@@ -3592,19 +3724,19 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
 #endif
     if (step_fused) {
         if (timing) DS.ev_kind.back() |= 32;          // (no K1 kernel: K1 runs inside the step)
-        if (tall) (void)hipEventRecord(ev[0], st);
+        if (tall) (void)hipEventRecord(ev(0), st);
         // K1 takes 16 lanes for each of the block's spb_f scenes, K2 spb_f x C lanes: the block needs
         // both (C <= 9 gives cg.threads < 16 spb_f; the K1 of the scenes beyond would not run)
         const int threads_f = step_waves == 1 ? 256 : step_waves == 2 ? 512
                                                       : std::max(cg.threads, ((16 * spb_f + 63) / 64) * 64);
         // the step kernel's own start/end timestamps go into K2's events (the launch's dispatch
         // records them): no marker packets in the stream, which cost a few us each in a ~0.1 ms step
-        hipEvent_t e1 = tk2 ? ev[1] : nullptr, e2 = tk2 ? ev[2] : nullptr;
+        hipEvent_t e1 = tk2 ? ev(1) : nullptr, e2 = tk2 ? ev(2) : nullptr;
         if (fio) {
-            if (tk2) (void)hipEventRecord(ev[1], st);
+            if (tk2) (void)hipEventRecord(ev(1), st);
             hipLaunchKernelGGL(k_plan_frame, dim3(1), dim3(threads_f), lds_f, st, *fio, mg, B, P, pv, R, spb_f,
                                rec, adjm, step_waves == 1 ? 1 : 0);
-            if (tk2) (void)hipEventRecord(ev[2], st);
+            if (tk2) (void)hipEventRecord(ev(2), st);
         } else if (step_waves == 2) {
             hipExtLaunchKernelGGL(k_step_small512, dim3((unsigned)groups_f), dim3(threads_f), (uint32_t)lds_f, st,
                                   e1, e2, 0u, mg, B, P, pv, R, spb_f, rec, adjm);
@@ -3612,13 +3744,14 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             hipExtLaunchKernelGGL(k_step_small, dim3((unsigned)groups_f), dim3(threads_f), (uint32_t)lds_f, st,
                                   e1, e2, 0u, mg, B, P, pv, R, spb_f, rec, adjm, step_waves == 1 ? 1 : 0);
         }
-        if (tall) (void)hipEventRecord(ev[3], st);
+        if (tall) (void)hipEventRecord(ev(3), st);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
     if (hipMemsetAsync(gb.count, 0, kSplitMax * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     const bool split = ref_direct && !P.emit_paths && !fused && cg.bps == 1 && Dn == 1 &&
                        prep_group(Sv) == 1 && split_on(S);
+    g_dbg[PP_DBG_LAST_PARTS].store(split ? split_parts(S) : 1, std::memory_order_relaxed);
     if (split) {
         // split_parts(S) parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
         // their scenes, part 0 on the caller's stream, part h > 0 on stream st2[h - 1]; each part
@@ -3647,8 +3780,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             GroupBits gbh = gb;
             gbh.count = gb.count + h;
             gbh.list = gb.list + g0;
-            hipEvent_t* eh = ev + 4 * h;
-            if (tall) (void)hipEventRecord(eh[0], sh);
+            const int eh = 4 * h;
+            if (tall) (void)hipEventRecord(ev(eh), sh);
             const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
             if (prep_w4(v1 - v0, device)) {
                 if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
@@ -3657,16 +3790,16 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                 if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
                 else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             }
-            if (tk2) (void)hipEventRecord(eh[1], sh);
+            if (tk2) (void)hipEventRecord(ev(eh + 1), sh);
             const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
             hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
             hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
                                cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
-            if (tk2) (void)hipEventRecord(eh[2], sh);
+            if (tk2) (void)hipEventRecord(ev(eh + 2), sh);
             hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
                                rec, adjm, v0, v1);
-            if (tall) (void)hipEventRecord(eh[3], sh);
+            if (tall) (void)hipEventRecord(ev(eh + 3), sh);
         }
         for (int k = 0; k < NP - 1; k++)
             if (hipEventRecord(W.join[k], W.st2[k]) != hipSuccess || hipStreamWaitEvent(st, W.join[k], 0) != hipSuccess)
@@ -3679,7 +3812,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         const int threads = 256;
         const int G = prep_group(Sv);
         const int64_t blocks = (Sv * G + threads - 1) / threads;
-        if (tall) (void)hipEventRecord(ev[0], st);
+        if (tall) (void)hipEventRecord(ev(0), st);
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
 #define PP_LAUNCH_PREP(KER) \
@@ -3708,7 +3841,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         const unsigned nb = (unsigned)cg.groups;
         const unsigned nslow = (unsigned)std::min<int64_t>(cg.groups, 2048);
         const int64_t ng = cg.groups;
-        if (tk2) (void)hipEventRecord(ev[1], st);
+        if (tk2) (void)hipEventRecord(ev(1), st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
         hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
                            cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0);          \
@@ -3723,7 +3856,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         else { PP_LAUNCH_CAND(0); }
 #undef PP_LAUNCH_CAND
     }
-    if (tk2) (void)hipEventRecord(ev[2], st);
+    if (tk2) (void)hipEventRecord(ev(2), st);
     // K4 (reference mode, winner-only output): replay the winners' recorded paths
     if (ref_direct && !P.emit_paths && !emit_in) {
         if (S <= kEmitSmall) {     // latency regime: 64-lane blocks over more CUs, 16 steps per load round
@@ -3740,7 +3873,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
         hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
     }
-    if (tall) (void)hipEventRecord(ev[3], st);
+    if (tall) (void)hipEventRecord(ev(3), st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
     return PP_OK;
 }
@@ -3761,7 +3894,7 @@ int32_t pp_debug_set(int32_t key, int32_t value) {
         case PP_DBG_SHAPE: ok = value >= 0 && value <= PP_SHAPE_STEP; break;
         case PP_DBG_POISON: ok = value == 0 || value == 1; break;
         case PP_DBG_SPLIT: ok = value >= 0 && value <= 2; break;
-        default: break;
+        default: break;       // (PP_DBG_LAST_PARTS is read-only)
     }
     if (!ok) return PP_ERR_ARG;
     g_dbg[key].store(value, std::memory_order_relaxed);
@@ -3776,8 +3909,9 @@ int32_t pp_timing_enable(pp_map* M, int32_t device, int32_t enable) {
     DevState& D = M->dev[device];
     D.timing = enable == PP_TIMING_K2 ? 2 : (enable != 0 ? 1 : 0);
     if (D.timing) {
-        // the events of 256 calls made now, outside any timed region (pp_eval takes 8 per call
-        // from the pool, pp_timing_read returns them)
+        // events made now, outside any timed region: 2,048 calls of K2-only timing (2 events each,
+        // 2 per part when split) or 1,024 of all-kernel timing (4 per part); pp_eval takes the
+        // events it records from this pool, pp_timing_read returns them
         DeviceGuard g(device);
         const int rc = dev_init(M, device);       // (pp_map_destroy frees the events of initialised devices)
         if (rc) return rc;
@@ -3801,6 +3935,7 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     const size_t ng = D.ev_rec.size() / EG;
     // signed milliseconds from a to b (either order)
     auto dt = [&](hipEvent_t a, hipEvent_t b, float& t) {
+        if (!a || !b) { rc = PP_ERR_HIP; return false; }
         if (hipEventElapsedTime(&t, a, b) == hipSuccess) return true;
         if (hipEventElapsedTime(&t, b, a) == hipSuccess) { t = -t; return true; }
         rc = PP_ERR_HIP;
@@ -3810,8 +3945,10 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
         const int kind = D.ev_kind[i], parts = (kind >> 1) & 7, np = parts ? parts : 1;
         const bool k2only = (kind & 16) != 0;
         hipEvent_t* e0 = &D.ev_rec[EG * i];
-        for (int h = 0; h < np; h++)
-            if (hipEventSynchronize(k2only ? e0[4 * h + 2] : e0[4 * h + 3]) != hipSuccess) rc = PP_ERR_HIP;
+        for (int h = 0; h < np; h++) {
+            hipEvent_t last = k2only ? e0[4 * h + 2] : e0[4 * h + 3];
+            if (!last || hipEventSynchronize(last) != hipSuccess) rc = PP_ERR_HIP;
+        }
         // stage k (0: K1, 1: K2, 2: K3/K4) of a call: from its earliest start to its latest end over
         // the parts (one stream: the kernel's own interval; a split call's parts overlap, and the
         // stage's time is the span they cover together, as in a kernel trace), one launch per call
@@ -3826,7 +3963,8 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
             }
             if (ok) { ms3[k] += hi - lo; launches3[k]++; }
         }
-        for (int k = 0; k < EG; k++) D.ev_pool.push_back(D.ev_rec[EG * i + k]);
+        for (int k = 0; k < EG; k++)
+            if (D.ev_rec[EG * i + k]) D.ev_pool.push_back(D.ev_rec[EG * i + k]);
     }
     D.ev_rec.clear();
     D.ev_kind.clear();

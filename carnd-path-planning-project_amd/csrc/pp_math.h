@@ -321,6 +321,15 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return r;
 }
 
+// 1/d to ~2^-48 relative: v_rcp_f64 (~2^-24: tools/rcp_check.hip) and one Newton step. Enough for
+// the Markstein quotient below: with r = (1 + e)/d its result carries ~e^2 = 2^-96 of relative error
+// before the final rounding, which is therefore the correct one (a quotient within 2^-96 of a
+// rounding midpoint is the only exception), exactly as with rcp_nr's r
+__device__ __forceinline__ double rcp_nr1(double d) {
+    const double r = __builtin_amdgcn_rcp(d);
+    return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+}
+
 // n / d from r ~ 1/d (within ~1 ulp): q0 = n r, then one Markstein correction with the exact
 // residual n - q0 d (fma). With r within half an ulp of 1/d (r = RN(1/d), e.g. 0.02 for 50) the
 // result is the correctly rounded quotient; with rcp_nr's r it is in all but rare cases (then one
@@ -394,6 +403,9 @@ __device__ __forceinline__ bool sqrt_rd(double q, double& d, double& rd) {
         rd = 2.0 * h;
         return true;
     }
+#ifdef PP_CENSUS
+    asm volatile(";@R 9 sqrtslow");      // (tools/valu_census.py region marker)
+#endif
     d = __builtin_sqrt(q);
     rd = 1.0 / d;
     return false;

@@ -18,6 +18,16 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PPAMD_LIB") or os.path.join(_HERE, "libppamd.so")   # override: A/B builds
 
+
+def lib_sha256(path=None):
+    """SHA-256 of the loaded HIP library file (bench.py matches profile summaries against it)."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(path or LIB_PATH, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
 def _open():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"ppamd: HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
@@ -552,7 +562,7 @@ DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
 TIMING_ALL, TIMING_K2 = 1, 2
 
 # pp_debug_set keys and launch shapes (include/pp.h PP_DBG_*, PP_SHAPE_*)
-DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT = 0, 1, 2, 3, 4
+DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT, DBG_LAST_PARTS = 0, 1, 2, 3, 4, 5
 SPLIT_AUTO, SPLIT_ON, SPLIT_OFF = 0, 1, 2
 SHAPE_AUTO, SHAPE_SPLIT, SHAPE_CAND_SMALL, SHAPE_STEP = 0, 1, 2, 3
 

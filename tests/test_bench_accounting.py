@@ -128,3 +128,35 @@ def test_rocprof_summarize_tool(tmp_path):
     assert out["launches_per_step"] == 1 and out["parts"] == 2 and out["dominant_launches"] == 3
     assert out["candidates_per_launch"] == 262144 * 15
     assert "k_prep<true, false>" in out["kernels"]
+
+
+def test_profile_entries_need_the_loaded_librarys_stamp():
+    """Counters and profiler durations measured on another library build describe another binary:
+    bench.py drops traffic, valu_roofline and frac_rocprof unless the entry's lib_sha256 is the
+    loaded library's, and records which entries it dropped."""
+    sha = "ab" * 32
+    pmc = {"candidates_per_launch": 10, "hbm_bytes_per_launch": 1.0, "lib_sha256": sha}
+    rp = {"dominant_ms_per_launch": 1.0, "lib_sha256": sha}
+    p, r, st = bench.profile_entries(pmc, rp, sha)
+    assert p is pmc and r is rp and st["pmc"] == "match" and st["rocprof"] == "match"
+    p, r, st = bench.profile_entries(pmc, dict(rp, lib_sha256="cd" * 32), sha)
+    assert p is pmc and r is None and st["rocprof"].startswith("stale")
+    p, r, st = bench.profile_entries({k: v for k, v in pmc.items() if k != "lib_sha256"}, None, sha)
+    assert p is None and r is None and st["pmc"].startswith("stale") and st["rocprof"] is None
+    assert bench.roofline_fields(p, 10, 1.0, 1.0) == (None, None)
+
+
+def test_shard_projection_arithmetic():
+    pr = bench.shard_projection(0.010, {2: 0.005, 4: 0.0026, 8: 0.00135})
+    assert pr["2"]["speedup"] == pytest.approx(2.0) and pr["2"]["efficiency"] == pytest.approx(1.0)
+    assert pr["8"]["speedup"] == pytest.approx(0.010 / 0.00135)
+    assert pr["8"]["efficiency"] == pytest.approx(0.010 / 0.00135 / 8)
+    assert pr["4"]["shard_ms_per_step"] == pytest.approx(2.6)
+
+
+def test_ppamd_and_tools_hash_the_same_library():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import shape_tags
+    from oracle_lib import ppamd
+    assert ppamd.lib_sha256() == shape_tags.lib_sha256(ppamd.LIB_PATH)

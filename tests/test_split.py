@@ -31,16 +31,21 @@ def run(env, sc, prm, mode):
     return ppamd.result_to_numpy(r)
 
 
-@pytest.mark.parametrize("S,mode", [(140000, ppamd.SPLIT_AUTO), (420000, ppamd.SPLIT_AUTO), (1048583, ppamd.SPLIT_AUTO),
-                                    (20000, ppamd.SPLIT_ON),
-                                    (20011, ppamd.SPLIT_ON)])
-def test_split_bit_identical(env, S, mode):
+# (S, mode, parts): the automatic split (131,072 to 1,572,864 scenes) and the forced one below its
+# range (more than 65,536 scenes: one K1 lane per scene); 70,013 = 17 * 4,118 + 7 leaves a partial
+# last group
+@pytest.mark.parametrize("S,mode,parts", [(140000, ppamd.SPLIT_AUTO, 2), (420000, ppamd.SPLIT_AUTO, 3),
+                                          (1048583, ppamd.SPLIT_AUTO, 3), (70001, ppamd.SPLIT_ON, 2),
+                                          (70013, ppamd.SPLIT_ON, 2)])
+def test_split_bit_identical(env, S, mode, parts):
     sc = ppamd.synth_host(env["m"], S, seed=S, first=S)
     idx = np.arange(7, S, 211)                    # speed-edge scenes: k_cand<true> groups in both halves
     sc["ego_speed_mph"][idx] = np.array([-0.0, 5e-324, 3e6, -3.0])[np.arange(len(idx)) % 4]
     prm = ppamd.default_params()
     a = run(env, sc, prm, mode)
+    assert ppamd.debug_get(ppamd.DBG_LAST_PARTS) == parts      # the split really ran
     b = run(env, sc, prm, ppamd.SPLIT_OFF)
+    assert ppamd.debug_get(ppamd.DBG_LAST_PARTS) == 1
     for k in a:
         x, y = np.asarray(a[k]), np.asarray(b[k])
         assert (x.view(np.uint8) == y.view(np.uint8)).all(), k

@@ -15,7 +15,9 @@ sys.path.insert(0, os.path.join(REPO, "carnd-path-planning-project_amd"))
 
 NAMES = ["step", "seg_reload", "ramp_div", "wide_turn", "limiter", "override", "curv_adjust",
          "override_cls1", "wide_first_step", "dt_le_0", "limiter_ng0", "limiter_ng1", "limiter_ng2_4",
-         "limiter_ng5_9", "limiter_ng10_19", "limiter_ng20_", "match_walk_step", "car_match"]
+         "limiter_ng5_9", "limiter_ng10_19", "limiter_ng20_", "match_walk_step", "car_match", "not_dok",
+         "adjust_wide", "loop_entry", "seg_back", "winner_out",
+         "adjust_narrow"]
 
 
 def main():
@@ -44,6 +46,7 @@ def main():
     assert lib.pp_diag_read(buf, 1) == 0
     lanes0, waves0 = buf[0], buf[1]
     out = {"scenes": S, "n_speeds": a.n_speeds, "n_points": a.n_points, "emit_paths": a.emit_paths, "lane_steps": lanes0, "wave_steps": waves0,
+           "waves": buf[2 * 20 + 1], "lanes": buf[2 * 20],
            "lanes_per_wave_step": lanes0 / max(waves0, 1)}
     for k, n in enumerate(NAMES):
         if not n or k == 0:

@@ -40,7 +40,7 @@ def main(a, b):
             print("only-in-new", k)
             bad += 1
         elif ka[k] == kb[k]:
-            print("same", len(ka[k]), k)
+            print("same", len(ka[k] or []), k)
         else:
             n = sum(1 for x, y in zip(ka[k], kb[k]) if x != y) + abs(len(ka[k]) - len(kb[k]))
             print("DIFFERENT", len(ka[k]), len(kb[k]), n, k)

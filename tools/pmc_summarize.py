@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-from shape_tags import DOMINANT, parse_tag
+from shape_tags import DOMINANT, lib_sha256, parse_tag
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 tag = sys.argv[2] if len(sys.argv) > 2 else None
@@ -50,6 +50,6 @@ if tag:
             "pipeline_bytes_by_kernel": per_kernel,
             "fetch_kib_raw": fetch, "write_kib": write,
             "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), dominant-kernel instantiations summed",
-            "counters": kc})
+            "counters": kc, "lib_sha256": lib_sha256()})
         json.dump(out, open(p, "w"), indent=1)
         print("wrote", p, tag)

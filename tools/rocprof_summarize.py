@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-from shape_tags import DOMINANT, parse_tag
+from shape_tags import DOMINANT, lib_sha256, parse_tag
 
 
 def main():
@@ -61,7 +61,8 @@ def main():
     out = json.load(open(p)) if os.path.exists(p) else {}
     out[tag] = dict(shape, **{"launches_per_step": 1, "parts": parts, "dominant_ms_per_launch": dom_ms,
                               "dominant_launches": calls, "dominant_time": how, "kernels": kernels,
-                              "source": f"rocprofv3 --kernel-trace --stats of bench.py ({src}, summarised into profiles/)"})
+                              "source": f"rocprofv3 --kernel-trace --stats of bench.py ({src}, summarised into profiles/)",
+                              "lib_sha256": lib_sha256()})
     json.dump(out, open(p, "w"), indent=1, sort_keys=True)
     print("wrote", p, tag, f"dominant {dom_ms:.4f} ms per launch")
 

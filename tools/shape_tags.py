@@ -1,6 +1,22 @@
 """bench.py's launch-shape tags and the dominant kernel of a step (shared by pmc_summarize.py and
 rocprof_summarize.py)."""
+import hashlib
+import os
 import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT_LIB = os.path.join(REPO, "carnd-path-planning-project_amd", "ppamd", "libppamd.so")
+
+
+def lib_sha256(path=None):
+    """SHA-256 of the product library a profiled run loaded (PPAMD_LIB, else the in-tree build):
+    every summary entry carries it, and bench.py uses an entry's counters only for that library."""
+    path = path or os.environ.get("PPAMD_LIB") or DEFAULT_LIB
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
 
 # the dominant kernel of a step: k_cand (both instantiations); the small-batch shapes fuse it
 # into k_cand_small / k_step_small
