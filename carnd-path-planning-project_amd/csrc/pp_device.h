@@ -15,6 +15,10 @@
 #define PP_DIAGC(k, c) ((void)0)
 #endif
 
+#ifndef PP_WGRID
+#define PP_WGRID 1          // the closest-waypoint cell table (init_reference_waypoint); 0: A/B builds
+#endif
+
 namespace ppd {
 
 constexpr double kPi = 3.14159265358979323846;   // helpers.h:33
@@ -30,10 +34,20 @@ constexpr int kMapArrays = 4 + 5 * NL;
 // lden[lane*n+i] = (ax - bx)^2 + (ay - by)^2 for a = lc[i-1], b = lc[i]: distancesq_pt_seg's rdenom
 // (helpers.h:202) for that lane segment, and lrcp = RN(1 / lden). fastm: every lden lies in
 // [2^-500, 2^500] (no degenerate lane segment), so lane_matching may use the tables.
+// The closest-waypoint cell table (host build_wgrid): for a square cell of side 1 / ginv near the
+// road, the (at most 4) waypoints that can be the closest one to any point of the cell, ascending,
+// the last repeated; 0xFFFFFFFF in .x: no list (the full scan). Cell (i, j) at wgrid[j * gnx + i]
+// covers [gx0 + i / ginv, gx0 + (i + 1) / ginv) x [gy0 + j / ginv, ...).
+struct WGrid {
+    const uint2* cells = nullptr;
+    double gx0 = 0, gy0 = 0, ginv = 0;
+    int gnx = 0, gny = 0;
+};
 struct MapV {
     const double *ref_x, *ref_y, *nx, *ny, *lc_x, *lc_y, *llen, *lden, *lrcp;
     int n;
     int fastm;
+    WGrid wg;
 };
 
 // Per-scene preparation output of K1 (SoA, workspace).
@@ -106,12 +120,41 @@ __device__ inline void init_reference_waypoint(const MapV& m, double x, double y
                                                double ratio[NL]) {
     const int n = m.n;
     int closest = 0;
-    double cd;
-    { const double dx = m.ref_x[0] - x, dy = m.ref_y[0] - y; cd = dx * dx + dy * dy; }
-    for (int i = 1; i < n; i++) {
-        const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
-        const double d = dx * dx + dy * dy;
-        if (d < cd) { closest = i; cd = d; }
+    // the closest waypoint (:150-154): the first i with the smallest |ref_i - p|^2 (strict `d < cd`
+    // from d_0). Near the road the cell table holds every waypoint that can be it for a point of the
+    // cell (ascending): the same scan over them gives the same index, since the first minimal index
+    // of the whole map is among them and no smaller listed index reaches the minimum (build_wgrid);
+    // elsewhere (and for NaN or infinite positions) the full scan
+    bool scan = true;
+    if (PP_WGRID && m.wg.cells) {
+        const double fx = (x - m.wg.gx0) * m.wg.ginv, fy = (y - m.wg.gy0) * m.wg.ginv;
+        if (fx >= 0 && fy >= 0 && fx < (double)m.wg.gnx && fy < (double)m.wg.gny) {
+            const uint2 c = m.wg.cells[(int64_t)(int)fy * m.wg.gnx + (int)fx];
+            if (c.x != 0xFFFFFFFFu) {
+                scan = false;
+                const int i0 = (int)(c.x & 0xFFFFu), i1 = (int)(c.x >> 16), i2 = (int)(c.y & 0xFFFFu),
+                          i3 = (int)(c.y >> 16);
+                double cd;
+                { const double dx = m.ref_x[i0] - x, dy = m.ref_y[i0] - y; cd = dx * dx + dy * dy; }
+                closest = i0;
+                const int ix[3] = {i1, i2, i3};
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const double dx = m.ref_x[ix[k]] - x, dy = m.ref_y[ix[k]] - y;
+                    const double d = dx * dx + dy * dy;
+                    if (d < cd) { closest = ix[k]; cd = d; }
+                }
+            }
+        }
+    }
+    if (scan) {
+        double cd;
+        { const double dx = m.ref_x[0] - x, dy = m.ref_y[0] - y; cd = dx * dx + dy * dy; }
+        for (int i = 1; i < n; i++) {
+            const double dx = m.ref_x[i] - x, dy = m.ref_y[i] - y;
+            const double d = dx * dx + dy * dy;
+            if (d < cd) { closest = i; cd = d; }
+        }
     }
     init_reference_waypoint_from(m, x, y, closest, ref_wp, ratio);
 }

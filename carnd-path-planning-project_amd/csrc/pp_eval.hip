@@ -115,7 +115,7 @@ using namespace ppd;
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
 // kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL] lden[NL] lrcp[NL]
-struct MapG { const double* buf; int n; int fastm; };
+struct MapG { const double* buf; int n; int fastm; WGrid wg; };
 
 // |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
 // <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
@@ -881,7 +881,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
 #ifdef PP_TRACE
     if (threadIdx.x == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1)) trace_at(kTraceK1 + blockIdx.x, 1);
 #endif
-    const MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
+    MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
+    m.wg = mg.wg;                         // the closest-waypoint cell table (global memory)
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
@@ -3022,6 +3023,7 @@ struct StreamWS {
 struct DevState {
     bool init = false;
     double* map = nullptr;        // kMapArrays * n
+    uint2* wgrid = nullptr;       // the closest-waypoint cell table (pp_map::wgrid)
     double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
@@ -3053,6 +3055,8 @@ struct pp_map {
     std::vector<double> ptab;     // (4 + 2 NL) * n: ref xy, normal, lane centres (pp_map_geometry)
     std::vector<double> lanetab;  // 5 NL * n
     int fastm = 0;                // MapV::fastm: bit 1: every lane segment's rdenom in [2^-500, 2^500]; bit 2: approach_seg's map bounds
+    std::vector<uint2> wgrid;     // closest-waypoint cell table (build_wgrid; empty: none)
+    WGrid wg;                     // its geometry (cells: the device copy, set per device)
     DevState dev[kMaxDev];
     std::mutex mu;
 };
@@ -3084,6 +3088,92 @@ void fill_ptab(pp_map* M) {
     for (size_t i = (size_t)(4 + 3 * NL) * n; i < (size_t)(4 + 4 * NL) * n; i++) appr = appr && g[i] >= 1.0;
     for (size_t i = (size_t)4 * n; i < (size_t)(4 + 2 * NL) * n; i++) appr = appr && std::fabs(g[i]) < 4e4;
     if (appr) M->fastm |= 2;
+}
+
+// The closest-waypoint cell table (pp_device.h WGrid, init_reference_waypoint). Cells of 16 m
+// within 32 m of the waypoint polyline get a list: waypoint w can be the closest one to a point of
+// cell B only if its distance to B, dmin(w, B), is at most U = min over all waypoints of the
+// largest distance from w' to B (the closest waypoint of any point of B is at most U away). B is
+// grown by 0.5 m on each side (the kernel's cell index rounds), and the test carries a relative
+// margin of 1e-6 (the kernel's squared distances round by a few ulps): the list holds every
+// waypoint that can be the scan's answer. Lists of up to 4 (the highway map's cells near the road
+// hold 1-4); a cell with more, or away from the road, has none (0xFFFFFFFF: the kernel scans).
+// Maps of more than 65,535 waypoints, or whose table would take more than 5e7 distance tests to
+// build, get no table.
+void build_wgrid(pp_map* M) {
+    constexpr double kCell = 16.0, kNear = 32.0, kGrow = 0.5;
+    const int n = M->n;
+    M->wgrid.clear();
+    M->wg = WGrid{};
+    if (n < 1 || n > 65535) return;
+    const double* rx = M->geom.data();
+    const double* ry = rx + n;
+    double x0 = rx[0], x1 = rx[0], y0 = ry[0], y1 = ry[0];
+    for (int i = 0; i < n; i++) {
+        if (!std::isfinite(rx[i]) || !std::isfinite(ry[i])) return;
+        x0 = std::min(x0, rx[i]); x1 = std::max(x1, rx[i]); y0 = std::min(y0, ry[i]); y1 = std::max(y1, ry[i]);
+    }
+    const double gx0 = x0 - 2 * kNear, gy0 = y0 - 2 * kNear;
+    const double wdt = x1 - x0 + 4 * kNear, hgt = y1 - y0 + 4 * kNear;
+    if (!(wdt / kCell < 1e5 && hgt / kCell < 1e5)) return;
+    const int gnx = (int)std::ceil(wdt / kCell), gny = (int)std::ceil(hgt / kCell);
+    // cells near the polyline: sample every segment every 2 m, mark cells within kNear
+    std::vector<uint8_t> near((size_t)gnx * gny, 0);
+    const int R = (int)std::ceil(kNear / kCell);
+    for (int i = 0; i < n; i++) {
+        const int j = (i + 1) % n;
+        const double len = std::hypot(rx[j] - rx[i], ry[j] - ry[i]);
+        const int ns = std::max(1, (int)std::ceil(len / 2.0));
+        for (int k = 0; k <= ns; k++) {
+            const double t = (double)k / ns;
+            const double px = rx[i] + (rx[j] - rx[i]) * t, py = ry[i] + (ry[j] - ry[i]) * t;
+            const int ci = (int)((px - gx0) / kCell), cj = (int)((py - gy0) / kCell);
+            for (int dj = -R; dj <= R; dj++)
+                for (int di = -R; di <= R; di++) {
+                    const int a = ci + di, b = cj + dj;
+                    if (a >= 0 && b >= 0 && a < gnx && b < gny) near[(size_t)b * gnx + a] = 1;
+                }
+        }
+    }
+    size_t nnear = 0;
+    for (uint8_t v : near) nnear += v;
+    if ((double)nnear * n > 5e7) return;
+    std::vector<uint2> cells((size_t)gnx * gny, uint2{0xFFFFFFFFu, 0xFFFFFFFFu});
+    std::vector<int> cand;
+    for (int cj = 0; cj < gny; cj++)
+        for (int ci = 0; ci < gnx; ci++) {
+            if (!near[(size_t)cj * gnx + ci]) continue;
+            const double bx0 = gx0 + ci * kCell - kGrow, bx1 = gx0 + (ci + 1) * kCell + kGrow;
+            const double by0 = gy0 + cj * kCell - kGrow, by1 = gy0 + (cj + 1) * kCell + kGrow;
+            double U = INFINITY;
+            for (int i = 0; i < n; i++) {
+                const double fx = std::max(std::fabs(rx[i] - bx0), std::fabs(rx[i] - bx1));
+                const double fy = std::max(std::fabs(ry[i] - by0), std::fabs(ry[i] - by1));
+                U = std::min(U, fx * fx + fy * fy);
+            }
+            const double lim = U * (1 + 1e-6) + 1e-6;
+            cand.clear();
+            for (int i = 0; i < n && cand.size() <= 4; i++) {
+                const double dx = std::max({bx0 - rx[i], rx[i] - bx1, 0.0});
+                const double dy = std::max({by0 - ry[i], ry[i] - by1, 0.0});
+                if (dx * dx + dy * dy <= lim) cand.push_back(i);
+            }
+            if (cand.empty() || cand.size() > 4) continue;
+            while (cand.size() < 4) cand.push_back(cand.back());
+            cells[(size_t)cj * gnx + ci] = uint2{(uint32_t)cand[0] | ((uint32_t)cand[1] << 16),
+                                                 (uint32_t)cand[2] | ((uint32_t)cand[3] << 16)};
+        }
+    M->wgrid.swap(cells);
+    M->wg.gx0 = gx0; M->wg.gy0 = gy0; M->wg.ginv = 1.0 / kCell; M->wg.gnx = gnx; M->wg.gny = gny;
+}
+
+// the device copy of the cell table (dev_init, pp_map_create_device)
+int upload_wgrid(pp_map* M, DevState& D) {
+    if (M->wgrid.empty()) return PP_OK;
+    if (hipMalloc(&D.wgrid, sizeof(uint2) * M->wgrid.size()) != hipSuccess) return PP_ERR_NOMEM;
+    if (hipMemcpy(D.wgrid, M->wgrid.data(), sizeof(uint2) * M->wgrid.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return PP_ERR_HIP;
+    return PP_OK;
 }
 
 // Map::Init (src/main.cpp:89-131) + derived tables, on the host (done once per map).
@@ -3130,6 +3220,7 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
         }
     }
     fill_ptab(M);
+    build_wgrid(M);
     M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     double* t = M->lanetab.data();
     for (int r = 0; r < NL; r++)
@@ -3183,6 +3274,8 @@ int dev_init(pp_map* M, int device) {
     if (hipMalloc(&D.lanetab, sizeof(double) * M->lanetab.size()) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemcpy(D.map, M->geom.data(), sizeof(double) * M->geom.size(), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
     if (hipMemcpy(D.lanetab, M->lanetab.data(), sizeof(double) * M->lanetab.size(), hipMemcpyHostToDevice) != hipSuccess) return PP_ERR_HIP;
+    const int rc = upload_wgrid(M, D);
+    if (rc != PP_OK) return rc;
     D.init = true;
     return PP_OK;
 }
@@ -3537,6 +3630,12 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
         return rc;
     }
     fill_ptab(M);
+    build_wgrid(M);
+    if (upload_wgrid(M, D) != PP_OK) {
+        (void)hipFree(D.map); (void)hipFree(D.lanetab);
+        delete M;
+        return PP_ERR_NOMEM;
+    }
     D.init = true;
     *out = M;
     return PP_OK;
@@ -3550,6 +3649,7 @@ int32_t pp_map_destroy(pp_map* M) {
         DeviceGuard g(d);
         (void)hipDeviceSynchronize();
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
+        if (D.wgrid) (void)hipFree(D.wgrid);
         for (auto& kv : D.sws) free_ws(kv.second);
         D.sws.clear();
         if (D.frame) (void)hipFree(D.frame);
@@ -3683,6 +3783,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.buf = DS.map;
     mg.n = M->n;
     mg.fastm = M->fastm;
+    mg.wg = M->wg;
+    mg.wg.cells = DS.wgrid;
     // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two).
     // The call's record is a group of 4 kSplitMax slots (before K1, after K1, after K2, after
     // K3/K4, per part); a slot takes an event from the pool when it is first recorded, so a
