@@ -18,6 +18,9 @@
 #ifndef PP_WGRID
 #define PP_WGRID 1          // the closest-waypoint cell table (init_reference_waypoint); 0: A/B builds
 #endif
+#ifndef PP_KDIV
+#define PP_KDIV 1           // K1's table reciprocals (project_speed, lane matching's last quotient)
+#endif
 
 namespace ppd {
 
@@ -48,6 +51,10 @@ struct MapV {
     int n;
     int fastm;
     WGrid wg;
+    // reference segments (build_wseg): wseg[b] = (|ref_b - ref_{b-1}|, RN(1 / that)), the length
+    // Map::project_speed computes (src/main.cpp:339) and its correctly rounded reciprocal; null:
+    // computed in place
+    const double2* wseg = nullptr;
 };
 
 // Per-scene preparation output of K1 (SoA, workspace).
@@ -425,7 +432,8 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
         const double rn = pdx * dx + pdy * dy;
         const double snom = pdx * dy - pdy * dx;
         const double rnom = rn < -1 ? 0.0 : (rn > den ? den : rn);
-        const double rfs = rnom / den;
+        // rnom / den by the table's RN(1 / den) (div_by_rcp: the correctly rounded quotient)
+        const double rfs = PP_KDIV ? div_by_rcp(rnom, den, m.lrcp[l * n + k_b]) : rnom / den;
         const double r_mod = rfs - k_sr;
         const double seg_len = m.llen[l * n + k_b];
         out_s = k_ss + seg_len * r_mod;
@@ -451,15 +459,25 @@ __device__ inline void project_speed(const MapV& m, double vx, double vy, int ne
     const int n = m.n;
     const int a = wpi(next_wp - 1, n), b = wpi(next_wp, n);
     double wx = m.ref_x[b] - m.ref_x[a], wy = m.ref_y[b] - m.ref_y[a];
+    double2 ws = {0, 0};
+    if (PP_KDIV && m.wseg) ws = m.wseg[b];              // (loaded ahead of the sqrt below)
     const double svl = sqrt(vx * vx + vy * vy);
     if (svl < kEps) {
         vs = svl;
         vd = 0;
         return;
     }
-    const double wvl = sqrt(wx * wx + wy * wy);
-    wx *= svl / wvl;
-    wy *= svl / wvl;
+    double q;
+    if (PP_KDIV && m.wseg) {
+        // wvl = sqrt(wx^2 + wy^2) is the table's (the host computes it with the same operations,
+        // correctly rounded sqrt), svl / wvl by its RN(1 / wvl): the same bits
+        q = div_by_rcp(svl, ws.x, ws.y);
+    } else {
+        const double wvl = sqrt(wx * wx + wy * wy);
+        q = svl / wvl;
+    }
+    wx *= q;
+    wy *= q;
     double sign = 1.0;
     if (wx * vx + wy * vy < 0) { vx *= -1; vy *= -1; sign = -1; }
     double rnom, rdenom, snom;

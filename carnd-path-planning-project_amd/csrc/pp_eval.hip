@@ -51,8 +51,10 @@ __device__ __forceinline__ void diag(int k, bool c) {
 // each region of the candidate loop; tools/valu_census.py counts each region's instructions in the
 // build's ISA and multiplies them by how often a wave executes the region (tools/diag_events.py)
 #define PP_REGION(name) asm volatile(";@R %0 " name ::"i"(kOutMode))
+#define PP_REGION_K(name) asm volatile(";@R 7 " name)
 #else
 #define PP_REGION(name) ((void)0)
+#define PP_REGION_K(name) ((void)0)
 #endif
 #ifdef PP_CHECK
 // checking builds only (-DPP_CHECK): every global store of k_cand / k_emit (and the record reads
@@ -115,7 +117,7 @@ using namespace ppd;
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
 // kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL] lden[NL] lrcp[NL]
-struct MapG { const double* buf; int n; int fastm; WGrid wg; };
+struct MapG { const double* buf; int n; int fastm; WGrid wg; const double2* wseg; };
 
 // |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
 // <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
@@ -319,6 +321,12 @@ constexpr int kWalkPf = 4;         // segments of the control-point walk loaded 
 constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
 #ifndef PP_CAND_WAVES
 #define PP_CAND_WAVES 4
+#endif
+#ifndef PP_CAND_WAVES2
+#define PP_CAND_WAVES2 PP_CAND_WAVES    // the all-paths instantiation k_cand<., 2>
+#endif
+#ifndef PP_ASIN_S
+#define PP_ASIN_S 0
 #endif
 constexpr int kCandWaves = PP_CAND_WAVES;   // k_cand waves per SIMD (<= 128 VGPRs)
 // Winner record (k_cand -> k_emit), room = N - K steps of scene s, rstride = room S: point-major
@@ -783,7 +791,11 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
         double ts, tt, fvx, fvy;
         bool col;
         car_velocity(in, P, S, s, draw, tab, fit, fvx, fvy);
+#ifdef PP_ABL_NOLIM
+        ts = fs; tt = fvx; col = false; const int code = 0;   // (ablation build: wrong results)
+#else
         const int code = limit_speed(P, fvx, fvy, fs, e.ego_s, e.ego_speed, e.ego_acc, in_lane, ts, tt, col);
+#endif
         status |= limit_flag(code) | (col ? PP_ST_COLLISION : 0u);
         if (t == 0) { pv.in_ts[v] = ts; pv.in_tt[v] = tt; }
         else { pv.l_ts[(t - 1) * Sv + v] = ts; pv.l_tt[(t - 1) * Sv + v] = tt; }
@@ -825,7 +837,11 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     // more (only from an absurd telemetry yaw) are outside the restated reduction.
     if (!gb.pose_by_wave) {
         double tv[4];
+#ifdef PP_ABL_NOTRIG
+        tv[0] = tv[2] = angle; tv[1] = tv[3] = -angle;           // (ablation build: wrong results)
+#else
         frame_trig<G>(angle, r, tv);
+#endif
         double* const tdst[4] = {pv.ca_m, pv.sa_m, pv.ca_p, pv.sa_p};
 #pragma unroll
         for (int t = 0; t < 4; t++)
@@ -883,6 +899,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
 #endif
     MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
     m.wg = mg.wg;                         // the closest-waypoint cell table (global memory)
+    m.wseg = mg.wseg;                     // reference segment lengths and reciprocals (global memory)
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
@@ -895,7 +912,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     const int draw = (int)(v - s * D);
 
     EgoSt e;
+    PP_REGION_K("ego");
     prep_ego<1>(m, in, P, S, s, 0, e);
+    PP_REGION_K("sort");
     uint32_t status = e.status;
     const int T_in = in.prev_target_lane[s];
     PlanAcc a;
@@ -916,7 +935,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     // sentinel), the identity order is kept. (more than 16 rows: the identity order)
     uint64_t order = 0xFEDCBA9876543210ull;
     bool sorted = false;
+#ifdef PP_ABL_NOSORT
+    if (false) {
+#else
     if (!tab && iters > 1 && iters <= 16) {
+#endif
         uint32_t key[16];
         bool neg = false;
 #pragma unroll
@@ -953,6 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     static_assert(PP_MAX_CARS <= (1 << PlanAcc::kItBits), "iteration index fields");
     int p = 0;                              // next unread row (table mode)
     for (int kk = 0; kk < iters; kk++) {
+        PP_REGION_K("carload");
         const int it = sorted ? (int)((order >> (4 * kk)) & 15) : kk;
         int row = it;
         const int64_t tix = (int64_t)it * S + s;
@@ -972,12 +996,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
             if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
             int nwp = 0;
             PP_DIAGC(17, true);
+            PP_REGION_K("match");
             if (!lane_match(m, e.ref_wp, e.ratio, cx, cy, cs, cd, clane, nwp)) {
                 status |= PP_ST_CAR_UNMATCHED;
                 if (tab) in.tab_valid[tix] = 0;
                 continue;
             }
+            PP_REGION_K("proj");
+#ifdef PP_ABL_NOPROJ
+            cvs = cvx; cvd = cvy;                                 // (ablation build: wrong results)
+#else
             project_speed(m, cvx, cvy, nwp, cvs, cvd);
+#endif
             if (tab) {
                 in.tab_valid[tix] = 1; in.tab_lane[tix] = clane;
                 in.tab_s[tix] = cs; in.tab_d[tix] = cd; in.tab_vs[tix] = cvs; in.tab_vd[tix] = cvd;
@@ -989,8 +1019,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
             clane = in.tab_lane[tix];
             cs = in.tab_s[tix]; cd = in.tab_d[tix]; cvs = in.tab_vs[tix]; cvd = in.tab_vd[tix];
         }
+        PP_REGION_K("plan");
+#ifdef PP_ABL_NOPLAN
+        a.nmatched += id + clane; a.in_s += cs + cd + cvs + cvd;  // (ablation build: wrong results)
+#else
         a.add(P, e, T_in, it, id, cs, cd, clane, cvs, cvd);
+#endif
     }
+    PP_REGION_K("finish");
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
 #ifdef PP_TRACE
     if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1))
@@ -1703,7 +1739,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_DIAGC(9, !(dt > 0));
         if (__builtin_expect(PP_NARROW(dt, cr), 1)) {
             PP_REGION("asin");
-            adiff = ((ppm::asin_small(cr) + 3 * kPi) - 2 * kPi) - kPi;
+            adiff = (((PP_ASIN_S == 2 ? ppm::asin_small_b(cr) : PP_ASIN_S ? ppm::asin_small_s(cr) : ppm::asin_small(cr)) + 3 * kPi) - 2 * kPi) - kPi;
         } else {
             PP_REGION("wide");
             // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
@@ -2192,7 +2228,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
 // are block-uniform; a barrier separates consecutive groups' use of the block's LDS). Each group
 // clears its bit after use, so the bitmap is all zero again for the next pp_eval.
 template <bool kSlow, int kMode>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kCandWaves))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES2 : kCandWaves))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
                                               uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
                                               const uint32_t* gcount, int64_t g0) {
@@ -3024,6 +3060,7 @@ struct DevState {
     bool init = false;
     double* map = nullptr;        // kMapArrays * n
     uint2* wgrid = nullptr;       // the closest-waypoint cell table (pp_map::wgrid)
+    double2* wseg = nullptr;      // reference segment lengths and reciprocals (pp_map::wseg)
     double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
@@ -3056,6 +3093,7 @@ struct pp_map {
     std::vector<double> lanetab;  // 5 NL * n
     int fastm = 0;                // MapV::fastm: bit 1: every lane segment's rdenom in [2^-500, 2^500]; bit 2: approach_seg's map bounds
     std::vector<uint2> wgrid;     // closest-waypoint cell table (build_wgrid; empty: none)
+    std::vector<double2> wseg;    // reference segment lengths and reciprocals (build_wseg; empty: none)
     WGrid wg;                     // its geometry (cells: the device copy, set per device)
     DevState dev[kMaxDev];
     std::mutex mu;
@@ -3167,12 +3205,39 @@ void build_wgrid(pp_map* M) {
     M->wg.gx0 = gx0; M->wg.gy0 = gy0; M->wg.ginv = 1.0 / kCell; M->wg.gnx = gnx; M->wg.gny = gny;
 }
 
-// the device copy of the cell table (dev_init, pp_map_create_device)
+// Map::project_speed's segment length (src/main.cpp:332-339: w = ref_b - ref_{b-1}, |w| =
+// sqrt(wx^2 + wy^2), the same operations as the kernel, unfused, correctly rounded sqrt) and
+// RN(1 / |w|) by IEEE division, per segment b (project_speed then divides by the reciprocal with one
+// Markstein correction: the correctly rounded quotient, ppd::div_by_rcp). Only for maps whose
+// lengths all lie in [2^-500, 2^500] (div_by_rcp's divisor range); else none.
+void build_wseg(pp_map* M) {
+    const int n = M->n;
+    M->wseg.clear();
+    const double* rx = M->geom.data();
+    const double* ry = rx + n;
+    std::vector<double2> t(n);
+    for (int b = 0; b < n; b++) {
+        const int a = (int)(((int64_t)b - 1 + n) % n);
+        const double wx = rx[b] - rx[a], wy = ry[b] - ry[a];
+        const double wvl = std::sqrt(wx * wx + wy * wy);
+        if (!(wvl >= 0x1p-500 && wvl <= 0x1p500)) return;
+        t[b] = double2{wvl, 1.0 / wvl};
+    }
+    M->wseg.swap(t);
+}
+
+// the device copies of the cell table and the segment table (dev_init, pp_map_create_device)
 int upload_wgrid(pp_map* M, DevState& D) {
-    if (M->wgrid.empty()) return PP_OK;
-    if (hipMalloc(&D.wgrid, sizeof(uint2) * M->wgrid.size()) != hipSuccess) return PP_ERR_NOMEM;
-    if (hipMemcpy(D.wgrid, M->wgrid.data(), sizeof(uint2) * M->wgrid.size(), hipMemcpyHostToDevice) != hipSuccess)
-        return PP_ERR_HIP;
+    if (!M->wgrid.empty()) {
+        if (hipMalloc(&D.wgrid, sizeof(uint2) * M->wgrid.size()) != hipSuccess) return PP_ERR_NOMEM;
+        if (hipMemcpy(D.wgrid, M->wgrid.data(), sizeof(uint2) * M->wgrid.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return PP_ERR_HIP;
+    }
+    if (!M->wseg.empty()) {
+        if (hipMalloc(&D.wseg, sizeof(double2) * M->wseg.size()) != hipSuccess) return PP_ERR_NOMEM;
+        if (hipMemcpy(D.wseg, M->wseg.data(), sizeof(double2) * M->wseg.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return PP_ERR_HIP;
+    }
     return PP_OK;
 }
 
@@ -3221,6 +3286,7 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
     }
     fill_ptab(M);
     build_wgrid(M);
+    build_wseg(M);
     M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     double* t = M->lanetab.data();
     for (int r = 0; r < NL; r++)
@@ -3631,6 +3697,7 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
     }
     fill_ptab(M);
     build_wgrid(M);
+    build_wseg(M);
     if (upload_wgrid(M, D) != PP_OK) {
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
         delete M;
@@ -3650,6 +3717,7 @@ int32_t pp_map_destroy(pp_map* M) {
         (void)hipDeviceSynchronize();
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
         if (D.wgrid) (void)hipFree(D.wgrid);
+        if (D.wseg) (void)hipFree(D.wseg);
         for (auto& kv : D.sws) free_ws(kv.second);
         D.sws.clear();
         if (D.frame) (void)hipFree(D.frame);
@@ -3785,6 +3853,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.fastm = M->fastm;
     mg.wg = M->wg;
     mg.wg.cells = DS.wgrid;
+    mg.wseg = DS.wseg;
     // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two).
     // The call's record is a group of 4 kSplitMax slots (before K1, after K1, after K2, after
     // K3/K4, per part); a slot takes an event from the pool when it is first recorded, so a
@@ -4464,6 +4533,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
     // (each field's bytes rounded out to whole 16-B units: the extra words are other fields of the
     // frame — inputs the kernel overwrites nothing of, outputs the host does not read — and a unit
     // range touching the previous one joins it)
+    bool fio_full = false;        // a range beyond the kernel argument's kFioMax (never: 15 in, 10 out)
     auto add = [&](bool in, const void* p, size_t bytes) {
         if (!bytes) return;
         const size_t b0 = (size_t)((const char*)p - (const char*)&h);
@@ -4475,6 +4545,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
             if (u1 > off[n - 1] + len[n - 1]) len[n - 1] = u1 - off[n - 1];
             return;
         }
+        if (n >= kFioMax) { fio_full = true; return; }
         off[n] = u0; len[n] = u1 - u0;
         n++;
     };
@@ -4496,6 +4567,7 @@ int32_t pp_plan_frame(pp_map* M, int32_t device, double ego_x, double ego_y, dou
                   offsetof(Frame, cost) == offsetof(Frame, ny) + sizeof(double) * N &&
                   offsetof(Frame, cid) == offsetof(Frame, nprev) + 12 && sizeof(pp_scene_info) % 4 == 0,
                   "adjacent frame fields");
+    if (fio_full) return PP_ERR_STATE;
     {   // the input units in range order, inline where they fit
         int nu = 0;
         for (int r = 0; r < io.n_in; r++) nu += (int)io.in_len[r];

@@ -313,6 +313,40 @@ __device__ __forceinline__ double asin_small(double s) {
     p = fma3(z, p, c1);
     return __builtin_fma(s * z, p, s);
 }
+// asin_small with its coefficients materialised in scalar registers at the use (PP_ASIN_S): the
+// loop then holds no coefficient in vector registers (12 VGPRs), at one v_mov_b64 for the first
+// term (a VOP3 reads one scalar operand)
+__device__ __forceinline__ double kcs(double v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ double fma_vvs(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+// the same with compiler-visible fused multiply-adds and constants (no inline-asm hazard padding)
+__device__ __forceinline__ double asin_small_b(double s) {
+    const double z = s * s;
+    double p = __builtin_fma(z, 1.73527644230769230769e-02, 2.23721590909090909091e-02);
+    p = __builtin_fma(z, p, 3.03819444444444444444e-02);
+    p = __builtin_fma(z, p, 4.46428571428571428571e-02);
+    p = __builtin_fma(z, p, 7.50000000000000000000e-02);
+    p = __builtin_fma(z, p, 1.66666666666666666667e-01);
+    return __builtin_fma(s * z, p, s);
+}
+__device__ __forceinline__ double asin_small_s(double s) {
+    const double z = s * s;
+    double c6 = kcs(1.73527644230769230769e-02);
+    asm volatile("" : "+v"(c6));
+    double p = fma_vvs(z, c6, kcs(2.23721590909090909091e-02));
+    p = fma_vvs(z, p, kcs(3.03819444444444444444e-02));
+    p = fma_vvs(z, p, kcs(4.46428571428571428571e-02));
+    p = fma_vvs(z, p, kcs(7.50000000000000000000e-02));
+    p = fma_vvs(z, p, kcs(1.66666666666666666667e-01));
+    return __builtin_fma(s * z, p, s);
+}
+
 // 1/d to ~1 ulp: v_rcp_f64 and two Newton steps (d finite, normal)
 __device__ __forceinline__ double rcp_nr(double d) {
     double r = __builtin_amdgcn_rcp(d);
