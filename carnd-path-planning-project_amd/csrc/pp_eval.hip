@@ -52,7 +52,9 @@ __device__ __forceinline__ void diag(int k, bool c) {
 // build's ISA and multiplies them by how often a wave executes the region (tools/diag_events.py)
 #define PP_REGION(name) asm volatile(";@R %0 " name ::"i"(kOutMode))
 #define PP_REGION_K(name) asm volatile(";@R 7 " name)
+#define PP_REGION_A(name) asm volatile(";@R 8 " name)
 #else
+#define PP_REGION_A(name) ((void)0)
 #define PP_REGION(name) ((void)0)
 #define PP_REGION_K(name) ((void)0)
 #endif
@@ -2023,8 +2025,10 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         const int L = j % NL;
         const int64_t s = s0 + j / NL;
         LaneGeom g;
+        PP_REGION_A("a1");
         if (act) { g = lane_geom(pv, s * D, Sv, L); team_a1(m, in, g, s, L, sl, r, TS); }
         __syncthreads();
+        PP_REGION_A("a2");
         // the two serial steps (A2, A4) on one lane per slot, slots in lane order: NL * SPB <= 64
         // slots fit the block's first wave, whose instruction stream is then the only one paying
         // for them (a team layout spreads them over every wave of the block)
@@ -2040,12 +2044,16 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             team_a2(gs, sls);
         }
         __syncthreads();
+        PP_REGION_A("a3");
         if (act) team_a3(sl, r, TS);
         __syncthreads();
+        PP_REGION_A("a4");
         if (act_s) team_a4(sls);
         __syncthreads();
+        PP_REGION_A("a5");
         if (act) team_a5(sl, r, TS);
     }
+    PP_REGION_A("pre");
     __syncthreads();
     if (!kSlow && tid == 0) PP_TRACE_AT(blockIdx.x, 1);
     // Lane -> candidate. Reference mode without draws (kMode 1): lanes [0, nsc) run the scenes'
@@ -2160,8 +2168,12 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         } else if (kMode == 1 && tid < 64) {
             // reference mode, the block's first wave: the winners record their local path
             // (3 stores per step) for k_emit; the other lanes of the wave are cost-only
+#ifdef PP_DIAG_NOB
+            R = CandRes{0, 0, N - K, 0, 0, 0};   // (diagnostic builds: phase B skipped)
+#else
             R = run_candidate<kSlow, 3>(P, sl, 0, 0, 0, 1, 0, sc, N - K, nullptr, nullptr,
                                                        S, nullptr, 0, winner, rec + s, 0, s);
+#endif
             if (winner && emit_in) {          // in-block K4 below: step count and masks in LDS
                 out.n_out[s] = K + R.ng;
                 out.winner[s] = c;
@@ -2173,10 +2185,15 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
                 adjm[S + s] = R.adj1;
             }
         } else {
+#ifdef PP_DIAG_NOB
+            R = CandRes{0, 0, N - K, 0, 0, 0};   // (diagnostic builds: phase B skipped)
+#else
             R = run_candidate<kSlow, 0>(P, sl, 0, 0, 0, 1, 0, sc, N - K,
                                                        nullptr, nullptr, 0, nullptr, 0, true, nullptr,
                                                        fabs(sc.target - sc.start) >= 7.5 * sc.ttime ? 2 : (sc.target > sc.start ? 1 : 0));
+#endif
         }
+        PP_REGION_A("post");
         uint32_t flags = R.flags;
         const double cost = cand_cost(P, R, K, pv.score[L * Sv + v], L, T, vt, pv.open_mask[v],
                                       pv.ego_lane[v], flags);
