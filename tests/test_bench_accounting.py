@@ -39,13 +39,16 @@ def test_paths_traffic_covers_the_written_paths(tag):
 
 
 def test_config5_entry_scales_to_shards():
+    """A shard size with its own profiled entry uses it (the 8-GPU shard, 262,144 scenes, round 5);
+    another size of the same shape scales the largest profiled launch per candidate."""
     e = PMC["k_cand_S2097152_C15_N50"]
-    pmc = bench.pmc_for(PMC, 262144, 15, 50, False, 1)      # an 8-GPU shard of config 5
+    assert bench.pmc_for(PMC, 262144, 15, 50, False, 1) is PMC.get("k_cand_S262144_C15_N50", e)
+    pmc = bench.pmc_for(PMC, 131072, 15, 50, False, 1)      # an unprofiled shard size
     assert pmc is e
     t_full, _ = bench.roofline_fields(pmc, 2097152 * 15, 104.3, 1.0)
-    t_shard, _ = bench.roofline_fields(pmc, 262144 * 15, 104.3, 1.0)
+    t_shard, _ = bench.roofline_fields(pmc, 131072 * 15, 104.3, 1.0)
     assert t_full == pytest.approx(e["hbm_bytes_per_launch"])
-    assert t_shard == pytest.approx(t_full / 8)
+    assert t_shard == pytest.approx(t_full / 16)
 
 
 def test_unprofiled_shape_has_no_traffic_and_unsized_entry_fails():
@@ -160,3 +163,12 @@ def test_ppamd_and_tools_hash_the_same_library():
     import shape_tags
     from oracle_lib import ppamd
     assert ppamd.lib_sha256() == shape_tags.lib_sha256(ppamd.LIB_PATH)
+
+
+def test_committed_summaries_are_stamped():
+    """Every committed PMC and kernel-trace summary entry names the library build it measured
+    (64 hex digits); bench.py uses an entry only while that build is the loaded one."""
+    import re
+    for name, d in (("pmc_summary.json", PMC), ("rocprof_summary.json", bench.load_rocprof_all())):
+        for tag, e in d.items():
+            assert re.fullmatch(r"[0-9a-f]{64}", str(e.get("lib_sha256"))), (name, tag)
