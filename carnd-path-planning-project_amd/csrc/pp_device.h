@@ -66,10 +66,27 @@ struct PrepV {
 };
 
 // src/main.cpp:134-137 (idx + size) % size, size_t arithmetic
-__device__ __forceinline__ int wpi(int idx, int n) {
-    if (idx >= 0) return idx < n ? idx : idx % n;
-    if (idx >= -n) return idx + n;
+__device__ __attribute__((noinline)) int wpi_far(int idx, int n) {
+    if (idx >= 0) return idx % n;
     return (int)(((uint64_t)(int64_t)idx + (uint64_t)n) % (uint64_t)n);
+}
+// Every index the walks form lies within one map length of [0, n) (a walk steps one waypoint at a
+// time from a valid index; the prefetches look a few waypoints ahead), where the wrap is one
+// compare and one add or subtract. Further out (tiny maps, walks round the loop) the integer
+// remainder, out of line: inline, the compiler evaluated its ~12-instruction sequence for every
+// index and selected the result (PP_WPI_FAST=0 keeps that form)
+#ifndef PP_WPI_FAST
+#define PP_WPI_FAST 1
+#endif
+__device__ __forceinline__ int wpi(int idx, int n) {
+    if (!PP_WPI_FAST) {
+        if (idx >= 0) return idx < n ? idx : idx % n;
+        if (idx >= -n) return idx + n;
+        return (int)(((uint64_t)(int64_t)idx + (uint64_t)n) % (uint64_t)n);
+    }
+    const int hi = idx - n, lo = idx + n;
+    if (__builtin_expect(idx >= -n && hi < n, 1)) return idx < 0 ? lo : (idx < n ? idx : hi);
+    return wpi_far(idx, n);
 }
 __device__ __forceinline__ double lane_offset(int lane) { return 4.0 * (lane + 0.5); }  // :84-88
 __device__ __forceinline__ double s_min(double a, double b) { return (b < a) ? b : a; }  // std::min

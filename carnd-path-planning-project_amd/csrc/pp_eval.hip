@@ -268,6 +268,12 @@ __device__ __forceinline__ double turn_angle_fast(double nc, double speed, doubl
 #ifndef PP_RCP1
 #define PP_RCP1 0
 #endif
+// PP_PRED (A/B switch, k_cand<false> cost-only and all-paths loops): the speed override and the
+// curvature adjustment as straight-line code with selects instead of exec-mask branches —
+// 1: inside the limiter branch, 2: on every step
+#ifndef PP_PRED
+#define PP_PRED 0
+#endif
 #ifndef PP_DT_NARROW
 #define PP_DT_NARROW 0
 #endif
@@ -928,7 +934,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     // either reported this frame (re-matched; slot overwritten, or erased when matching fails,
     // src/main.cpp:1329-1348) or taken from its stale slot.
     const bool tab = in.tab_valid != nullptr;
+#ifdef PP_ABL_NOCARS
+    const int iters = 0;                    // (ablation build: wrong results)
+#else
     const int iters = tab ? in.tab_slots : ncar;
+#endif
     // Visiting order (PlanAcc: any order once ties compare the iteration index). Without a car
     // table the rows are visited nearest first (squared distance to the ego, a 4-bit row index in
     // the low mantissa bits of a float key, sorted by a Batcher network): the k-th visit of every
@@ -1754,6 +1764,36 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
         PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
         PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
+#if PP_PRED
+        const bool lim_p = acc + cacc > P.maximum_acc;
+        if (!kLarge && (kOutMode == 0 || kOutMode == 4) && (PP_PRED == 2 || lim_p)) {
+            PP_REGION("pred");
+            // the same operations as the branches below, every lane; the results kept by selects
+            const bool up = lim_p && speed > prev_speed;
+            const double na = __builtin_fmax(P.maximum_acc - cacc, 0.0);
+            const double ns = prev_speed + PP_DIV50(na);
+            SC so = sc;
+            sc_override_r<kLarge>(so, cur_t, ns, rds);
+            so.ttime += 0.02;
+            const double rtt2 = PP_RCP1 ? ppm::rcp_nr1(so.ttime) : ppm::rcp_nr(so.ttime);
+            const double dstep2 = PP_DIV50(ns);
+            if (up) { sc = so; speed = ns; rtt = rtt2; dstep = dstep2; acc = na; R.flags |= PP_ST_ACC_OVERRIDE; }
+            const bool adj = lim_p && acc + cacc > P.maximum_acc;
+            const double nc = __builtin_fmax(P.maximum_acc - acc, 0.0);
+            if (kOutMode == 4) {
+                if (PP_NARROW(dt, cr)) {
+                    double ca2 = F.ca, sa2 = F.sa;
+                    turn_narrow(ca2, sa2, nc, speed, adiff, dt, cr);
+                    if (adj) { F.ca = ca2; F.sa = sa2; }
+                } else if (adj) {
+                    double crr, srr;
+                    turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), srr, crr);
+                    frame_rot(F.ca, F.sa, crr, srr);
+                }
+            }
+            if (adj) { eff_c = nc; R.flags |= PP_ST_CURV_ADJUST; }
+        } else
+#endif
         if (acc + cacc > P.maximum_acc) {
             PP_REGION("lim");
             if (speed > prev_speed) {                                   // :945-971
@@ -2026,7 +2066,9 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         const int64_t s = s0 + j / NL;
         LaneGeom g;
         PP_REGION_A("a1");
+#ifndef PP_SKIP_A1
         if (act) { g = lane_geom(pv, s * D, Sv, L); team_a1(m, in, g, s, L, sl, r, TS); }
+#endif
         __syncthreads();
         PP_REGION_A("a2");
         // the two serial steps (A2, A4) on one lane per slot, slots in lane order: NL * SPB <= 64
@@ -2041,17 +2083,25 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             gs.K = pv.K[vs];
             gs.npk = gs.K > 0 ? gs.K - 1 : 0;
             gs.pos_x = pv.pos_x[vs]; gs.pos_y = pv.pos_y[vs]; gs.ego_d = pv.ego_d[vs];
+#ifndef PP_SKIP_A2
             team_a2(gs, sls);
+#endif
         }
         __syncthreads();
         PP_REGION_A("a3");
+#ifndef PP_SKIP_A3
         if (act) team_a3(sl, r, TS);
+#endif
         __syncthreads();
         PP_REGION_A("a4");
+#ifndef PP_SKIP_A4
         if (act_s) team_a4(sls);
+#endif
         __syncthreads();
         PP_REGION_A("a5");
+#ifndef PP_SKIP_A5
         if (act) team_a5(sl, r, TS);
+#endif
     }
     PP_REGION_A("pre");
     __syncthreads();
