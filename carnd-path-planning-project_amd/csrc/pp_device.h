@@ -55,7 +55,17 @@ struct MapV {
     // Map::project_speed computes (src/main.cpp:339) and its correctly rounded reciprocal; null:
     // computed in place
     const double2* wseg = nullptr;
+    // the approach table (pp_eval.hip build_atab): kAtabD doubles per lane segment b, used where
+    // atab_on (k_prep: in LDS when the map is, so that its loads are LDS loads)
+    const double* atab = nullptr;
+    bool atab_on = false;
 };
+// approach table row b (the lane segments from waypoint b - 1 to b): dx_l, dy_l at 2 l, 2 l + 1 (the
+// walk's own RN(pb - pa)), kf_l at 2 NL + l, kb_l at 3 NL + l, the segment length llen_l at 4 NL + l
+// (l < NL)
+constexpr int kAtabD = (5 * NL + 1) & ~1;
+// margin of the certain approach test, m^2 (approach_cert)
+constexpr double kAtabMargin = 1e-3;
 
 // Per-scene preparation output of K1 (SoA, workspace).
 struct PrepV {
@@ -324,6 +334,34 @@ __device__ __forceinline__ bool approach_seg(const MapV& m, int a, int b, double
     }
     return fwd ? okf : okb;
 }
+// A *certain* approach segment (MapV::atab; maps with fastm bit 2, a point within 5e4 m of the
+// origin): per lane, t = x dx + y dy - k by two fmas, k = pa.d + rdenom + kAtabMargin (forward) or
+// pa.d - 1 - kAtabMargin (backward), d = (dx, dy). In real arithmetic t is the walk's rn - rdenom -
+// kAtabMargin (forward; rn + 1 + kAtabMargin backward) up to the roundings of k and of the two fmas;
+// under the fastm bounds (|x|, |y| < 5e4, lane centres within 4e4, |d| < 8e4) those and the walk's
+// own rounding of rn stay below 2e-5 m^2, far inside the margin: t > 0 (t < 0 backward) implies the
+// walk's rn > rdenom (rn < -1) for every lane, i.e. approach_seg. A segment it does not certify is
+// left to the full walk (approach runs stop there), which is always exact.
+__device__ __forceinline__ bool approach_cert(const MapV& m, int b, double x, double y, bool fwd) {
+    const double* r = m.atab + b * kAtabD;
+    const double* kr = r + (fwd ? 2 * NL : 3 * NL);
+    double d[2 * NL], k[NL];
+#pragma unroll
+    for (int l = 0; l < 2 * NL; l++) d[l] = r[l];
+#pragma unroll
+    for (int l = 0; l < NL; l++) k[l] = kr[l];
+    const double sg = fwd ? 1.0 : -1.0;     // (t sg > 0: exact, and false for t = 0 either way)
+    bool ok = true;
+#pragma unroll
+    for (int l = 0; l < NL; l++) ok &= __builtin_fma(x, d[2 * l], __builtin_fma(y, d[2 * l + 1], -k[l])) * sg > 0;
+    return ok;
+}
+#ifndef PP_ATAB
+#define PP_ATAB 1
+#endif
+__device__ __forceinline__ bool approach_test(const MapV& m, int a, int b, double x, double y, bool fwd) {
+    return (PP_ATAB && m.atab_on) ? approach_cert(m, b, x, y, fwd) : approach_seg(m, a, b, x, y, fwd);
+}
 // commits approach segments from iteration `it` (segment (a, b), an approach segment) while the
 // next one is one too; returns the iteration the full walk resumes at (its segment uncommitted).
 // After the walk's first step the ratio shift sr is 0 forward and 1 backward, so a commit adds or
@@ -336,13 +374,16 @@ __device__ __forceinline__ int approach_walk(const MapV& m, double x, double y, 
         if (it + 2 >= 4 * n + 8 || cur - 2 < -n) break;
         const int a2 = fwd ? b : (a == 0 ? n - 1 : a - 1);
         const int b2 = fwd ? (b + 1 == n ? 0 : b + 1) : a;
-        if (!approach_seg(m, a2, b2, x, y, fwd)) break;
-        PP_DIAGC(16, true);
+        // the committed segment's lengths, read before the test (with the table: from its row, in
+        // the same round trip to LDS as the tested row)
+        double len[NL];
 #pragma unroll
-        for (int l = 0; l < NL; l++) {
-            const double len = m.llen[l * n + b];
-            sum_s[l] += fwd ? len : -len;
-        }
+        for (int l = 0; l < NL; l++)
+            len[l] = (PP_ATAB && m.atab_on) ? m.atab[b * kAtabD + 4 * NL + l] : m.llen[l * n + b];
+        if (!approach_test(m, a2, b2, x, y, fwd)) break;
+        PP_DIAGC(24, true);
+#pragma unroll
+        for (int l = 0; l < NL; l++) sum_s[l] += fwd ? len[l] : -len[l];
         cur += dir;
         a = a2; b = b2;
         it++;
@@ -436,7 +477,7 @@ __device__ inline bool lane_matching_tab2(const MapV& m, int ref_wp, const doubl
             if (__builtin_expect(cur - 1 < -n, 0)) { a = wpi(cur - 1, n); b = wpi(cur, n); }
         }
         if (it == 0 && (m.fastm & 2) && fabs(x) < 5e4 && fabs(y) < 5e4 &&
-            approach_seg(m, a, b, x, y, dir > 0))
+            approach_test(m, a, b, x, y, dir > 0))
             it = approach_walk(m, x, y, dir, a, b, cur, sum_s, it + 1) - 1;
     }
     if (found) {                                                   // :214-227, last improvement

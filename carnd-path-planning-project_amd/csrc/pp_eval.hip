@@ -119,7 +119,9 @@ using namespace ppd;
 // K1: scene preparation
 // ------------------------------------------------------------------------------------------------
 // kMapArrays arrays of n: ref_x ref_y nx ny lc_x[NL] lc_y[NL] llen[NL] lden[NL] lrcp[NL]
-struct MapG { const double* buf; int n; int fastm; WGrid wg; const double2* wseg; };
+// atab: the approach table (global memory; build_atab; null: none); atab_lds: it fits k_prep<true,
+// false>'s LDS after the map (that kernel stages it there: the host passes it only then)
+struct MapG { const double* buf; int n; int fastm; WGrid wg; const double2* wseg; const double* atab; int atab_lds; };
 
 // |angle| bound for the hot loop: the loop adds at most 2*pi per curvature adjustment over
 // <= PP_MAX_POINTS steps, which keeps every sin/cos argument below ppm::kMediumMax.
@@ -898,8 +900,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
         g_trace[8 * (kTraceK1 + blockIdx.x) + 7] = trace_hwid();
     }
 #endif
+    // the approach table: in LDS after the map (16-B aligned) in k_prep<true, false> (the host
+    // sizes the launch for it, or passes none), else in global memory
+#ifndef PP_ATAB_LDS
+#define PP_ATAB_LDS 1
+#endif
+    constexpr bool kAtabL = kLdsMap && !kW4 && PP_ATAB_LDS;
+    double* satab = smap + ((kMapArrays * n + 1) & ~1);
     if (kLdsMap) {
         stage_map(smap, mg.buf, kMapArrays * n);
+        if (kAtabL && mg.atab) stage_map(satab, mg.atab, kAtabD * n);
         __syncthreads();
     }
 #ifdef PP_TRACE
@@ -908,6 +918,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     MapV m = map_view(kLdsMap ? smap : mg.buf, n, mg.fastm);
     m.wg = mg.wg;                         // the closest-waypoint cell table (global memory)
     m.wseg = mg.wseg;                     // reference segment lengths and reciprocals (global memory)
+    m.atab = kAtabL ? satab : mg.atab;    // the approach table (LDS or global memory)
+    m.atab_on = mg.atab != nullptr;
     // one lane per evaluation v = s * D + d (scene s, Monte-Carlo draw d; D = 1 without noise):
     // inputs are read at scene s (stride S), the prep record is written at v (stride Sv)
     const int64_t S = in.n_scenes;
@@ -3128,6 +3140,7 @@ struct DevState {
     double* map = nullptr;        // kMapArrays * n
     uint2* wgrid = nullptr;       // the closest-waypoint cell table (pp_map::wgrid)
     double2* wseg = nullptr;      // reference segment lengths and reciprocals (pp_map::wseg)
+    double* atab = nullptr;       // the approach table (pp_map::atab)
     double* lanetab = nullptr;    // synth tables: lc_x[NL n] lc_y[NL n] seg_len[NL n] tan_x[NL n] tan_y[NL n]
     std::map<void*, StreamWS> sws;  // per hip_stream
     void* frame = nullptr;        // single-frame scratch (pp_plan_frame)
@@ -3161,6 +3174,7 @@ struct pp_map {
     int fastm = 0;                // MapV::fastm: bit 1: every lane segment's rdenom in [2^-500, 2^500]; bit 2: approach_seg's map bounds
     std::vector<uint2> wgrid;     // closest-waypoint cell table (build_wgrid; empty: none)
     std::vector<double2> wseg;    // reference segment lengths and reciprocals (build_wseg; empty: none)
+    std::vector<double> atab;     // lane matching's approach table (build_atab; empty: none)
     WGrid wg;                     // its geometry (cells: the device copy, set per device)
     DevState dev[kMaxDev];
     std::mutex mu;
@@ -3293,7 +3307,46 @@ void build_wseg(pp_map* M) {
     M->wseg.swap(t);
 }
 
-// the device copies of the cell table and the segment table (dev_init, pp_map_create_device)
+// Lane matching's approach table (pp_device.h approach_cert): per lane segment b (waypoint b - 1 to
+// b) and lane l, d = RN(pb - pa) (the walk's own differences), c = pa.d, and the certain test's
+// constants c + rdenom + kAtabMargin (forward) and c - 1 - kAtabMargin (backward), rdenom the map's
+// own table value. Only for maps with fastm bit 2 (the bounds its margin argument needs).
+void build_atab(pp_map* M) {
+    M->atab.clear();
+    if (!(M->fastm & 2)) return;
+    const int n = M->n;
+    const double* g = M->geom.data();
+    const double* lcx = g + 4 * (size_t)n;
+    const double* lcy = g + (4 + NL) * (size_t)n;
+    const double* llen = g + (4 + 2 * NL) * (size_t)n;
+    const double* lden = g + (4 + 3 * NL) * (size_t)n;
+    std::vector<double> t((size_t)kAtabD * n, 0.0);
+    for (int b = 0; b < n; b++) {
+        const int a = b == 0 ? n - 1 : b - 1;
+        double* r = &t[(size_t)kAtabD * b];
+        for (int l = 0; l < NL; l++) {
+            const double pax = lcx[(size_t)l * n + a], pay = lcy[(size_t)l * n + a];
+            const double dx = lcx[(size_t)l * n + b] - pax, dy = lcy[(size_t)l * n + b] - pay;
+            const double c = pax * dx + pay * dy;
+            r[2 * l] = dx;
+            r[2 * l + 1] = dy;
+            r[2 * NL + l] = c + lden[(size_t)l * n + b] + kAtabMargin;
+            r[3 * NL + l] = c - 1.0 - kAtabMargin;
+            r[4 * NL + l] = llen[(size_t)l * n + b];
+        }
+    }
+    M->atab.swap(t);
+}
+
+void free_map_tables(DevState& D) {
+    if (D.wgrid) (void)hipFree(D.wgrid);
+    if (D.wseg) (void)hipFree(D.wseg);
+    if (D.atab) (void)hipFree(D.atab);
+    D.wgrid = nullptr; D.wseg = nullptr; D.atab = nullptr;
+}
+
+// the device copies of the cell table, the segment table and the approach table (dev_init,
+// pp_map_create_device)
 int upload_wgrid(pp_map* M, DevState& D) {
     if (!M->wgrid.empty()) {
         if (hipMalloc(&D.wgrid, sizeof(uint2) * M->wgrid.size()) != hipSuccess) return PP_ERR_NOMEM;
@@ -3303,6 +3356,11 @@ int upload_wgrid(pp_map* M, DevState& D) {
     if (!M->wseg.empty()) {
         if (hipMalloc(&D.wseg, sizeof(double2) * M->wseg.size()) != hipSuccess) return PP_ERR_NOMEM;
         if (hipMemcpy(D.wseg, M->wseg.data(), sizeof(double2) * M->wseg.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return PP_ERR_HIP;
+    }
+    if (!M->atab.empty()) {
+        if (hipMalloc(&D.atab, sizeof(double) * M->atab.size()) != hipSuccess) return PP_ERR_NOMEM;
+        if (hipMemcpy(D.atab, M->atab.data(), sizeof(double) * M->atab.size(), hipMemcpyHostToDevice) != hipSuccess)
             return PP_ERR_HIP;
     }
     return PP_OK;
@@ -3354,6 +3412,7 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
     fill_ptab(M);
     build_wgrid(M);
     build_wseg(M);
+    build_atab(M);
     M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     double* t = M->lanetab.data();
     for (int r = 0; r < NL; r++)
@@ -3609,6 +3668,11 @@ CandGeom cand_geom(int C, int64_t S) {
 
 int n_draws(const pp_params* p) { return p->n_draws > 1 ? p->n_draws : 1; }
 
+// k_prep<true, false>'s LDS with the approach table after the map (MapG::atab_lds)
+size_t prep_lds_atab(int n) {
+    return sizeof(double) * (((kMapArrays * (size_t)n + 1) & ~(size_t)1) + kAtabD * (size_t)n);
+}
+
 
 bool params_ok(const pp_params* p) {
     return p && p->n_points > PP_PREV_KEEP && p->n_points <= PP_MAX_POINTS && p->n_speeds >= 1 &&
@@ -3765,7 +3829,9 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
     fill_ptab(M);
     build_wgrid(M);
     build_wseg(M);
+    build_atab(M);
     if (upload_wgrid(M, D) != PP_OK) {
+        free_map_tables(D);
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
         delete M;
         return PP_ERR_NOMEM;
@@ -3783,8 +3849,7 @@ int32_t pp_map_destroy(pp_map* M) {
         DeviceGuard g(d);
         (void)hipDeviceSynchronize();
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
-        if (D.wgrid) (void)hipFree(D.wgrid);
-        if (D.wseg) (void)hipFree(D.wseg);
+        free_map_tables(D);
         for (auto& kv : D.sws) free_ws(kv.second);
         D.sws.clear();
         if (D.frame) (void)hipFree(D.frame);
@@ -3921,6 +3986,9 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     mg.wg = M->wg;
     mg.wg.cells = DS.wgrid;
     mg.wseg = DS.wseg;
+    mg.atab = DS.atab;
+    // k_prep<true, false> stages the approach table after the map where both fit a block's 64 KB
+    mg.atab_lds = DS.atab && sizeof(double) * (((kMapArrays * (size_t)M->n + 1) & ~(size_t)1) + kAtabD * (size_t)M->n) <= 65536;
     // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two).
     // The call's record is a group of 4 kSplitMax slots (before K1, after K1, after K2, after
     // K3/K4, per part); a slot takes an event from the pool when it is first recorded, so a
@@ -4010,6 +4078,9 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             if (hipStreamWaitEvent(W.st2[k], W.fork, 0) != hipSuccess) return PP_ERR_HIP;
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
+        const size_t lds_a = lmap && mg.atab_lds ? prep_lds_atab(mg.n) : lds;    // k_prep<true, false>
+        MapG mga = mg;
+        if (!mg.atab_lds) mga.atab = nullptr;
         for (int h = 0; h < NP; h++) {
             hipStream_t sh = h == 0 ? st : W.st2[h - 1];
             const int64_t g0 = G * h / NP, g1 = G * (h + 1) / NP;
@@ -4025,7 +4096,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                 if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
                 else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             } else {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1);
                 else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
             }
             if (tk2) (void)hipEventRecord(ev(eh + 1), sh);
@@ -4053,6 +4124,9 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         if (tall) (void)hipEventRecord(ev(0), st);
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
+        const size_t lds_a = lmap && mg.atab_lds ? prep_lds_atab(mg.n) : lds;    // k_prep<true, false>
+        MapG mga = mg;
+        if (!mg.atab_lds) mga.atab = nullptr;
 #define PP_LAUNCH_PREP(KER) \
         if (lmap) hipLaunchKernelGGL(KER<true>, dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb); \
         else hipLaunchKernelGGL(KER<false>, dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb)
@@ -4066,7 +4140,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                     if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                     else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 } else {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds_a, st, mga, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                     else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
                 }
                 break;

@@ -10,6 +10,11 @@ these tests drive the cases the shortcut touches against the oracle under the st
     initial 1000^2, or the per-walk bound (5e4 m) disables the runs.
 The closed-loop tests (tests/test_rollout.py, tests/test_cartable.py) walk re-reported cars from a
 moving ego through the same code.
+Round 5: the one-lane K1 (k_prep) certifies approach segments from a per-map table by two fmas per
+lane with a 1e-3 m^2 margin (approach_cert) and leaves uncertified ones to the full walk; the
+grouped K1 of small batches keeps the exact test. test_certified_runs_vs_oracle forces the
+one-lane K1 at both of its builds (LDS table at 3 waves per SIMD, global-memory table at 4) and adds
+cars within 1e-3 m of a lane point's perpendicular, where the margin decides.
 The 40,000-waypoint loop of tests/test_maps.py has lane segments shorter than 1 m: there the map
 flag (fastm bit 2) turns the runs off and the full walk alone runs."""
 import numpy as np
@@ -42,7 +47,7 @@ def run_gpu(env, d, prm):
     return ppamd.result_to_numpy(r)
 
 
-def walk_scenes(env, S, seed, far=False):
+def walk_scenes(env, S, seed, far=False, edge=False):
     """Synthetic scenes whose cars sit k waypoints from the ego's nearest waypoint (k in
     [-45, 45], any lane, jittered along and across the lane); with far=True a third of the cars
     are moved 1e4 ... 1e7 m away in a random direction."""
@@ -64,6 +69,8 @@ def walk_scenes(env, S, seed, far=False):
             tx, ty = geo[i2, 0] - geo[i, 0], geo[i2, 1] - geo[i, 1]
             tl = np.hypot(tx, ty)
             a = rng.uniform(-0.5, 0.5) * tl
+            if edge and rng.random() < 0.5:      # at the lane point's perpendicular, within 1e-3 m
+                a = rng.choice([0.0, 1.0, -1.0]) * 10 ** rng.uniform(-9, -3)
             off = rng.choice([rng.uniform(-1.5, 1.5), rng.uniform(-9.0, 9.0)])
             sc["car_x"][j, s] = lx + a * tx / tl + off * nx
             sc["car_y"][j, s] = ly + a * ty / tl + off * ny
@@ -105,3 +112,28 @@ def test_walks_across_the_wrap_vs_oracle(env):
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sub, prm, info=False)
     e = oracle_lib.compare(got, ref)
     print(f"{len(near)} scenes near the wrap: max |dxy| {e:.3e} m")
+
+
+@pytest.mark.parametrize("waves", [3, 4])
+def test_certified_runs_vs_oracle(env, waves):
+    """The one-lane K1 (PP_DBG_PREP_GROUP 1) at 3 waves per SIMD (the approach table in LDS) and at
+    4 (in global memory), on long walks with half the cars at a lane point's perpendicular (along-
+    track offsets 0 and 1e-9 ... 1e-3 m) and on walks across the wrap: bit-identical with the oracle
+    (Frenet state of the ego included) and with the grouped K1, which walks every segment exactly."""
+    S = 3000
+    sc = walk_scenes(env, S, 9090 + waves, edge=True)
+    d = to_dev(env, sc)
+    prm = ppamd.default_params(emit_paths=True)
+    with ppamd.debug(ppamd.DBG_PREP_GROUP, 1):
+        with ppamd.debug(ppamd.DBG_PREP_WAVES, waves):
+            got = run_gpu(env, d, prm)
+    with ppamd.debug(ppamd.DBG_PREP_GROUP, 4):
+        grp = run_gpu(env, d, prm)
+    for k, v in got.items():
+        w = grp[k]
+        if v.dtype == np.float64:
+            v, w = v.view(np.uint64), w.view(np.uint64)
+        assert np.array_equal(v, w), k
+    ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+    e = oracle_lib.compare(got, ref)
+    print(f"one-lane K1 at {waves} waves, {S} scenes (cars at perpendiculars): max |dxy| {e:.3e} m")

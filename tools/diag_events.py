@@ -17,7 +17,7 @@ NAMES = ["step", "seg_reload", "ramp_div", "wide_turn", "limiter", "override", "
          "override_cls1", "wide_first_step", "dt_le_0", "limiter_ng0", "limiter_ng1", "limiter_ng2_4",
          "limiter_ng5_9", "limiter_ng10_19", "limiter_ng20_", "match_walk_step", "car_match", "not_dok",
          "adjust_wide", "loop_entry", "seg_back", "winner_out",
-         "adjust_narrow"]
+         "adjust_narrow", "match_approach_step"]
 
 
 def main():
@@ -51,7 +51,8 @@ def main():
     for k, n in enumerate(NAMES):
         if not n or k == 0:
             continue
-        out[n] = {"lane_frac": buf[2 * k] / max(lanes0, 1), "wave_frac": buf[2 * k + 1] / max(waves0, 1)}
+        out[n] = {"lane_frac": buf[2 * k] / max(lanes0, 1), "wave_frac": buf[2 * k + 1] / max(waves0, 1),
+                  "lanes": buf[2 * k], "waves": buf[2 * k + 1]}
     print(json.dumps(out, indent=1))
 
 
