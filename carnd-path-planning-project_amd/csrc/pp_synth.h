@@ -38,13 +38,25 @@ struct LaneTables {
     const double* tan_y;
 };
 
+// a ^ b ^ c: one v_bitop3_b32 on gfx950 (truth table 0x96), which the compiler does not form itself
+#ifndef PP_BITOP3
+#define PP_BITOP3 1
+#endif
+PP_HD inline uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && PP_BITOP3
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 PP_HD inline void philox_round(uint32_t ctr[4], const uint32_t key[2]) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * ctr[0];
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * ctr[2];
     const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
     const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    const uint32_t n0 = hi1 ^ ctr[1] ^ key[0];
-    const uint32_t n2 = hi0 ^ ctr[3] ^ key[1];
+    const uint32_t n0 = xor3(hi1, ctr[1], key[0]);
+    const uint32_t n2 = xor3(hi0, ctr[3], key[1]);
     ctr[0] = n0; ctr[1] = lo1; ctr[2] = n2; ctr[3] = lo0;
 }
 
