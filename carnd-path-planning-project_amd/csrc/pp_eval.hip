@@ -888,6 +888,9 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
 
 // kW4: the 4-waves-per-SIMD instantiation (<= 128 VGPRs): for batches whose wave count fills
 // whole rounds of 4 waves per SIMD better than of 3 (prep_w4 in pp_eval)
+#ifndef PP_SORT_DMAX
+#define PP_SORT_DMAX 16          // k_prep sorts a scene's rows nearest first below this many draws
+#endif
 template <bool kLdsMap, bool kW4 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : kPrepWaves))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb,
@@ -956,13 +959,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     // the low mantissa bits of a float key, sorted by a Batcher network): the k-th visit of every
     // lane of a wave then walks a similar number of lane segments in lane_matching, which is where
     // the divergence was. With a table, or a negative car id (the reference's -1 'no car'
-    // sentinel), the identity order is kept. (more than 16 rows: the identity order)
+    // sentinel), the identity order is kept. (more than 16 rows: the identity order.) So do
+    // Monte-Carlo batches of 16 draws or more: a wave's lanes are the draws of at most 4 scenes
+    // (v = s D + d), which visit the same rows in lockstep anyway
     uint64_t order = 0xFEDCBA9876543210ull;
     bool sorted = false;
 #ifdef PP_ABL_NOSORT
     if (false) {
 #else
-    if (!tab && iters > 1 && iters <= 16) {
+    if (!tab && iters > 1 && iters <= 16 && D < PP_SORT_DMAX) {
 #endif
         uint32_t key[16];
         bool neg = false;
@@ -1051,7 +1056,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
 #endif
     }
     PP_REGION_K("finish");
+#ifdef PP_ABL_NOFINISH
+    // (register-pressure experiment: the car pass's results stored, no finish; wrong results)
+    pv.in_ts[v] = a.in_s + a.next_s[0] + a.next_s[1] + a.next_s[2] + a.t_s[0] + a.t_s[1] + a.t_s[2] + e.ego_s;
+    pv.K[v] = a.open_m + a.in_id + a.t_id[0] + a.t_id[1] + a.t_id[2] + a.lane_speed[0] + a.lane_speed[1] +
+              a.lane_speed[2] + a.ls_set + (int)a.its + (int)(a.its >> 32) + a.nmatched + (int)status + T_in;
+#else
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
+#endif
 #ifdef PP_TRACE
     if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1))
         trace_at(kTraceK1 + blockIdx.x, 2 + (threadIdx.x >> 6));
