@@ -27,7 +27,7 @@ def cpu():
 def test_noise_generator_host_copy_matches_oracle(cpu):
     olib = cpu["olib"]
     rng = np.random.default_rng(7)
-    for _ in range(3000):
+    for _ in range(20000):
         seed = int(rng.integers(0, 2**63))
         scene = int(rng.integers(0, 2**40))
         d, j, q = int(rng.integers(1, 1024)), int(rng.integers(0, 16)), int(rng.integers(0, 4))
@@ -38,6 +38,27 @@ def test_noise_generator_host_copy_matches_oracle(cpu):
                   for s in range(40) for d in range(1, 26) for j in range(12) for q in range(4)])
     assert abs(g.mean()) < 0.02 and abs(g.std() - 1.0) < 0.02
     assert np.abs(g).max() <= 2 * np.sqrt(3) + 1e-12       # Irwin-Hall(4) support
+
+
+def test_irwin_hall_integer_sum_form():
+    """The library forms the noise from the integer sum of the four words (csrc/pp_synth.h
+    mc_gauss: (c0 + c1 + c2 + c3 - (2^33 - 2)) (sqrt(3) 2^-32)); the oracle keeps the definition's
+    form (sum of (c_i + 0.5) 2^-32, minus 2, times sqrt(3)). Every step of the definition's sum is
+    exact, so both are the same product rounded once: checked on 2e6 random words and on the
+    extremes."""
+    rng = np.random.default_rng(11)
+    c = rng.integers(0, 2**32, size=(4, 2_000_000), dtype=np.uint64).astype(np.float64)
+    ext = np.array([0.0, 1.0, 2.0**31 - 1, 2.0**31, 2.0**32 - 2, 2.0**32 - 1])
+    grid = np.stack(np.meshgrid(ext, ext, ext, ext, indexing="ij")).reshape(4, -1)
+    c = np.concatenate([c, grid], axis=1)
+    k = 1.0 / 4294967296.0
+    s = (c[0] + 0.5) * k
+    s = s + (c[1] + 0.5) * k
+    s = s + (c[2] + 0.5) * k
+    s = s + (c[3] + 0.5) * k
+    old = (s - 2.0) * 1.7320508075688772
+    new = (((c[0] + c[1]) + (c[2] + c[3])) - 8589934590.0) * (1.7320508075688772 * 2.0**-32)
+    assert np.array_equal(old.view(np.uint64), new.view(np.uint64))
 
 
 @pytest.mark.parametrize("mode,n_speeds,D", [(ppamd.COST_COMFORT, 2, 6), (ppamd.COST_REFERENCE, 1, 5)])
