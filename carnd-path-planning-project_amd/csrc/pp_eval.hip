@@ -880,10 +880,16 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
 __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int draw, int row, double& cx,
                                           double& cy, double& cvx, double& cvy) {
     const uint64_t gs = (uint64_t)(P.noise_first_scene + s);
-    cx += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 0);
-    cy += P.noise_pos_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 1);
-    cvx += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 2);
-    cvy += P.noise_vel_sigma * ppsynth::mc_gauss(P.noise_seed, gs, draw, row, 3);
+    double g[4];
+#ifndef PP_G4
+#define PP_G4 1
+#endif
+    if (PP_G4) ppsynth::mc_gauss4(P.noise_seed, gs, draw, row, g);      // (mc_gauss q = 0..3)
+    else for (int q = 0; q < 4; q++) g[q] = ppsynth::mc_gauss(P.noise_seed, gs, draw, row, q);
+    cx += P.noise_pos_sigma * g[0];
+    cy += P.noise_pos_sigma * g[1];
+    cvx += P.noise_vel_sigma * g[2];
+    cvy += P.noise_vel_sigma * g[3];
 }
 
 // kW4: the 4-waves-per-SIMD instantiation (<= 128 VGPRs): for batches whose wave count fills

@@ -79,6 +79,24 @@ static_assert(PP_MAX_CARS <= PP_NOISE_CAR_STRIDE, "noise counter stride below th
 #ifndef PP_IH_SUM
 #define PP_IH_SUM 1
 #endif
+// the Irwin-Hall sum of one Philox block's words, as (s - 2) sqrt(3) (mc_gauss)
+PP_HD inline double ih_unit(const uint32_t c[4]) {
+    // (s - 2) sqrt(3) with s = sum_i (c_i + 0.5) 2^-32: every partial sum of that s is exact (at most
+    // 35 significant bits), so s - 2 = (c_0 + c_1 + c_2 + c_3 - (2^33 - 2)) 2^-32 exactly; the
+    // integer sum is exact in doubles too, and scaling sqrt(3) by 2^-32 is exact: the one rounding
+    // left is the same product's
+#if PP_IH_SUM
+    const double t = (((double)c[0] + (double)c[1]) + ((double)c[2] + (double)c[3])) - 8589934590.0;
+    return t * (1.7320508075688772 * 0x1p-32);
+#else
+    const double k = 1.0 / 4294967296.0;
+    double s = ((double)c[0] + 0.5) * k;
+    s += ((double)c[1] + 0.5) * k;
+    s += ((double)c[2] + 0.5) * k;
+    s += ((double)c[3] + 0.5) * k;
+    return (s - 2.0) * 1.7320508075688772;
+#endif
+}
 PP_HD inline double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, int q) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     uint32_t ctr[4] = {(uint32_t)scene, (uint32_t)(scene >> 32), (uint32_t)(((draw * PP_NOISE_CAR_STRIDE) + car) * 4 + q), 0x4D43u};
@@ -87,21 +105,27 @@ PP_HD inline double mc_gauss(uint64_t seed, uint64_t scene, int draw, int car, i
         key[0] += 0x9E3779B9u;
         key[1] += 0xBB67AE85u;
     }
-    // (s - 2) sqrt(3) with s = sum_i (c_i + 0.5) 2^-32: every partial sum of that s is exact (at most
-    // 35 significant bits), so s - 2 = (c_0 + c_1 + c_2 + c_3 - (2^33 - 2)) 2^-32 exactly; the
-    // integer sum is exact in doubles too, and scaling sqrt(3) by 2^-32 is exact: the one rounding
-    // left is the same product's
-#if PP_IH_SUM
-    const double t = (((double)ctr[0] + (double)ctr[1]) + ((double)ctr[2] + (double)ctr[3])) - 8589934590.0;
-    return t * (1.7320508075688772 * 0x1p-32);
-#else
-    const double k = 1.0 / 4294967296.0;
-    double s = ((double)ctr[0] + 0.5) * k;
-    s += ((double)ctr[1] + 0.5) * k;
-    s += ((double)ctr[2] + 0.5) * k;
-    s += ((double)ctr[3] + 0.5) * k;
-    return (s - 2.0) * 1.7320508075688772;
-#endif
+    return ih_unit(ctr);
+}
+// the four draws of one car (q = 0..3: x, y, vx, vy noise) at once: the same four Philox blocks as
+// four mc_gauss calls, their rounds interleaved (independent chains)
+PP_HD inline void mc_gauss4(uint64_t seed, uint64_t scene, int draw, int car, double g[4]) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        ctr[q][0] = (uint32_t)scene; ctr[q][1] = (uint32_t)(scene >> 32);
+        ctr[q][2] = (uint32_t)(((draw * PP_NOISE_CAR_STRIDE) + car) * 4 + q); ctr[q][3] = 0x4D43u;
+    }
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) philox_round(ctr[q], key);
+        key[0] += 0x9E3779B9u;
+        key[1] += 0xBB67AE85u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) g[q] = ih_unit(ctr[q]);
 }
 
 struct Rng {
