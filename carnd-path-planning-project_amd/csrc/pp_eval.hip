@@ -270,12 +270,6 @@ __device__ __forceinline__ double turn_angle_fast(double nc, double speed, doubl
 #ifndef PP_RCP1
 #define PP_RCP1 0
 #endif
-// PP_PRED (A/B switch, k_cand<false> cost-only and all-paths loops): the speed override and the
-// curvature adjustment as straight-line code with selects instead of exec-mask branches —
-// 1: inside the limiter branch, 2: on every step
-#ifndef PP_PRED
-#define PP_PRED 0
-#endif
 #ifndef PP_DT_NARROW
 #define PP_DT_NARROW 0
 #endif
@@ -1062,14 +1056,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
 #endif
     }
     PP_REGION_K("finish");
-#ifdef PP_ABL_NOFINISH
-    // (register-pressure experiment: the car pass's results stored, no finish; wrong results)
-    pv.in_ts[v] = a.in_s + a.next_s[0] + a.next_s[1] + a.next_s[2] + a.t_s[0] + a.t_s[1] + a.t_s[2] + e.ego_s;
-    pv.K[v] = a.open_m + a.in_id + a.t_id[0] + a.t_id[1] + a.t_id[2] + a.lane_speed[0] + a.lane_speed[1] +
-              a.lane_speed[2] + a.ls_set + (int)a.its + (int)(a.its >> 32) + a.nmatched + (int)status + T_in;
-#else
     prep_finish<1>(in, P, pv, info, out_status, gb, S, Sv, s, v, draw, tab, 0, T_in, e, a, status);
-#endif
 #ifdef PP_TRACE
     if ((threadIdx.x & 63) == 0 && blockIdx.x < (unsigned)(kTraceMax - kTraceK1))
         trace_at(kTraceK1 + blockIdx.x, 2 + (threadIdx.x >> 6));
@@ -1794,36 +1781,6 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
         PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
         PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
-#if PP_PRED
-        const bool lim_p = acc + cacc > P.maximum_acc;
-        if (!kLarge && (kOutMode == 0 || kOutMode == 4) && (PP_PRED == 2 || lim_p)) {
-            PP_REGION("pred");
-            // the same operations as the branches below, every lane; the results kept by selects
-            const bool up = lim_p && speed > prev_speed;
-            const double na = __builtin_fmax(P.maximum_acc - cacc, 0.0);
-            const double ns = prev_speed + PP_DIV50(na);
-            SC so = sc;
-            sc_override_r<kLarge>(so, cur_t, ns, rds);
-            so.ttime += 0.02;
-            const double rtt2 = PP_RCP1 ? ppm::rcp_nr1(so.ttime) : ppm::rcp_nr(so.ttime);
-            const double dstep2 = PP_DIV50(ns);
-            if (up) { sc = so; speed = ns; rtt = rtt2; dstep = dstep2; acc = na; R.flags |= PP_ST_ACC_OVERRIDE; }
-            const bool adj = lim_p && acc + cacc > P.maximum_acc;
-            const double nc = __builtin_fmax(P.maximum_acc - acc, 0.0);
-            if (kOutMode == 4) {
-                if (PP_NARROW(dt, cr)) {
-                    double ca2 = F.ca, sa2 = F.sa;
-                    turn_narrow(ca2, sa2, nc, speed, adiff, dt, cr);
-                    if (adj) { F.ca = ca2; F.sa = sa2; }
-                } else if (adj) {
-                    double crr, srr;
-                    turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), srr, crr);
-                    frame_rot(F.ca, F.sa, crr, srr);
-                }
-            }
-            if (adj) { eff_c = nc; R.flags |= PP_ST_CURV_ADJUST; }
-        } else
-#endif
         if (acc + cacc > P.maximum_acc) {
             PP_REGION("lim");
             if (speed > prev_speed) {                                   // :945-971

@@ -23,7 +23,7 @@ REGION_EVENT = {"head": None, "seg": "seg_reload", "segback": "seg_back", "eval"
                 "dirfix": "not_dok", "cross": None, "asin": None, "wide": "wide_turn", "acc": None,
                 "lim": "limiter", "ovr": "override", "lim2": "limiter", "adj": "curv_adjust",
                 "adjwide": "adjust_wide", "adjn": "adjust_narrow", "sqrtslow": "not_dok", "tail": None, "tailfix": "not_dok", "tail2": None, "out": None,
-                "outw": "winner_out", "out2": None, "latch": None, "pred": "limiter"}
+                "outw": "winner_out", "out2": None, "latch": None}
 
 
 def classify(op):
