@@ -403,7 +403,9 @@ __device__ __forceinline__ void car_velocity(const pp_scene_batch& in, const pp_
 // kLimSlow scene in this bitmap for k_cand<true>
 // (list/count: the flagged groups in the order k_prep found them, for k_cand<true>; count is zeroed
 // before every K1)
-struct GroupBits { uint32_t* bits; int SPB, BPS; uint32_t* list; uint32_t* count; int pose_by_wave; };
+// (BPS < 0: the flat all-paths geometry, groups of 256 consecutive candidates of the batch, C per
+// scene: a scene lies in groups s C / 256 ... ((s + 1) C - 1) / 256)
+struct GroupBits { uint32_t* bits; int SPB, BPS; uint32_t* list; uint32_t* count; int pose_by_wave; int C; };
 // ---- K1 building blocks, shared by k_prep (one lane per evaluation) and k_prep_g2..16 (G lanes) ----
 
 // Ego state of one evaluation: derivation (src/main.cpp:1233-1292), Frenet frame and ego matching
@@ -828,8 +830,9 @@ __device__ __forceinline__ void prep_finish(const pp_scene_batch& in, const pp_p
     }
     if (!ok) lim_mask |= kLimSlow;
     if ((lim_mask & kLimSlow) && r == 0 && gb.bits) {   // (k_step_small: no bitmap)
-        const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : s * gb.BPS;
-        for (int b = 0; b < gb.BPS; b++) {
+        const int64_t g0 = gb.BPS == 1 ? s / gb.SPB : gb.BPS < 0 ? s * gb.C / 256 : s * gb.BPS;
+        const int nb = gb.BPS < 0 ? (int)(((s + 1) * gb.C - 1) / 256 - g0 + 1) : gb.BPS;
+        for (int b = 0; b < nb; b++) {
             const uint32_t bit = 1u << ((g0 + b) & 31);
             const uint32_t old = atomicOr(&gb.bits[(g0 + b) >> 5], bit);
             if (!(old & bit) && gb.list) gb.list[atomicAdd(gb.count, 1u)] = (uint32_t)(g0 + b);
@@ -2010,12 +2013,20 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     const int64_t S = in.n_scenes;
     const int64_t Sv = S * D;
     // block -> scenes: BPS == 1: SPB whole scenes; BPS > 1 (C > 256): one scene, candidates
-    // [coff, coff + 256) of it
+    // [coff, coff + 256) of it; BPS < 0 (kMode 2, the flat geometry): the batch's candidates
+    // [256 g, 256 g + 256), from candidate coff of scene s0 on, over at most SPB scenes
     int64_t s0;
     int coff;
+    int nsc;
     if (BPS == 1) { s0 = g * SPB; coff = 0; }
+    else if (BPS < 0) { s0 = g * 256 / C; coff = (int)(g * 256 - s0 * C); }
     else { s0 = g / BPS; coff = (int)(g - s0 * BPS) * 256; }
-    const int nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
+    if (BPS < 0) {
+        const int span = (coff + 255) / C + 1;
+        nsc = (int)((S - s0) < span ? (S - s0) : span);
+    } else {
+        nsc = (int)((S - s0) < SPB ? (S - s0) : SPB);
+    }
     const int tid = threadIdx.x;
     // per scene: any of its draws flagged kLimSlow (absurd heading, or a speed or ramp time outside
     // the range of the unchecked divisions) -> the scene runs in the k_cand<true> instantiation
@@ -3631,8 +3642,25 @@ size_t cand_geom_lds(int spb) {
     size_t lds = sizeof(double) * 5 * kKP * (size_t)nslot + sizeof(int) * 4 * nslot + sizeof(uint32_t) * 2 * spb;
     return ((lds + 7) & ~(size_t)7) + sizeof(uint64_t) * 2 * spb + sizeof(int) * spb;
 }
-CandGeom cand_geom(int C, int64_t S) {
+// the flat geometry for the all-paths mode (kMode 2): 256-lane groups over the batch's candidates,
+// scenes straddling two groups (their spline slots built in both, status flags merged with
+// atomics): four full waves per block where whole scenes would leave a wave slot of the CU idle
+// (C = 24: 8 scenes in 3 waves, 5 blocks = 15 of 16 waves per CU). Up to (C + 254) / C + 1 scenes
+// per group; C >= 13 keeps those slots within the first wave (NL SPB <= 64 for phase A's serial steps)
+#ifndef PP_CAND_FLAT
+#define PP_CAND_FLAT 1
+#endif
+bool cand_flat_ok(int C) { return PP_CAND_FLAT && C >= 13 && C <= 128 && 256 % C != 0; }
+CandGeom cand_geom(int C, int64_t S, bool flat = false) {
     CandGeom g;
+    if (flat) {
+        g.spb = (C + 254) / C + 1;
+        g.bps = -1;
+        g.threads = 256;
+        g.lds = cand_geom_lds(g.spb);
+        g.groups = (S * C + 255) / 256;
+        return g;
+    }
     g.spb = C <= 256 ? cands_per_block(C) : 1;
     g.bps = C <= 256 ? 1 : (C + 255) / 256;
     g.threads = C <= 256 ? ((g.spb * C + 63) / 64) * 64 : 256;
@@ -3885,7 +3913,8 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     // reference decision without draws: the winner is known before the loop (k_cand records it,
     // k_emit writes it); otherwise the decision is a cost argmin (k_winner)
     const bool ref_direct = prm->cost_mode == PP_COST_REFERENCE && Dn == 1;
-    const CandGeom cg = cand_geom(Dn * NL * prm->n_speeds, S);
+    const int Cn_ = Dn * NL * prm->n_speeds;
+    const CandGeom cg = cand_geom(Cn_, S, prm->emit_paths && Dn == 1 && cand_flat_ok(Cn_));
     if (cg.groups > 0x7fffffff) return PP_ERR_ARG;
     // small batches in reference mode without paths: K2 and K4 in one launch (k_cand_small, K4 in
     // the block: emit_in), unless the horizon's sin/cos table (2 N doubles per winner) exceeds the
@@ -3987,7 +4016,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     pp_result R = *out;
     if (!P.emit_paths) { R.paths = nullptr; R.path_len = nullptr; }
     GroupBits gb = {};
-    gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps;
+    gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps; gb.C = Cn_;
     gb.count = W.gbits + W.gbits_cap;
     gb.list = gb.count + kSplitMax;
 #ifdef PP_CHECK

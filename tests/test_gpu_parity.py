@@ -156,6 +156,27 @@ def test_speed_range_edges_vs_oracle(env, emit):
     print(f"speed edges (emit={emit}): max |dxy| {e:.3e} m")
 
 
+@pytest.mark.parametrize("n_speeds", [4, 6, 7, 8])
+def test_flat_groups_vs_oracle(env, n_speeds):
+    """All-paths mode in the flat k_cand geometry (round 5, pp_eval.hip cand_geom / cand_group:
+    groups of 256 consecutive candidates, scenes straddling two groups, their spline slots built in
+    both and their status flags merged with atomics): C = 18, 21, 24 straddle; C = 12 keeps whole
+    scenes per group. A third of the scenes carry speed-edge telemetry, so k_prep routes them to
+    k_cand<true> and marks every group they touch."""
+    S = 700
+    sc = ppamd.synth_host(env["m"], S, seed=4100 + n_speeds, first=999)
+    speeds = [-0.0, 5e-324, 1e-300, 1e-18, 3e6, -3.0]
+    for s in range(0, S, 3):
+        sc["n_prev"][s] = 0
+        sc["ego_speed_mph"][s] = speeds[(s // 3) % len(speeds)]
+    offs = [-6, -4, -3, -2, -1, 0, 2][:n_speeds - 1]
+    prm = ppamd.default_params(emit_paths=True, n_speeds=n_speeds, speed_offsets=offs)
+    got = run_gpu(env, to_dev(env, sc), prm)
+    ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
+    e = compare(got, ref)
+    print(f"flat groups, C = {3 * n_speeds}: max |dxy| {e:.3e} m")
+
+
 def test_device_synth_matches_host_synth(env):
     dev = ppamd.scenes_to_numpy(ppamd.synth_device(env["m"], 2000, seed=31, first=777, device=0))
     host = ppamd.synth_host(env["m"], 2000, seed=31, first=777)
