@@ -59,3 +59,27 @@ class TestMapsGPU:
         ref = oracle_lib.oracle_eval(oracle_lib.load_oracle(), wx, wy, ppamd.scenes_to_numpy(sc_dev), prm, info=False)
         e = compare(got, ref)
         assert e <= 1e-6, e
+
+    @pytest.mark.parametrize("n,waves", [(300, 3), (300, 4), (2000, 3), (2000, 4)])
+    def test_one_lane_k1_maps_vs_oracle(self, n, waves):
+        """The one-lane K1 (PP_DBG_PREP_GROUP 1) at both builds on maps where lane matching's
+        approach table (round 5, pp_device.h approach_cert) does not sit in LDS: 300 waypoints
+        (the map in LDS, map and table over a block's 64 KB: k_prep<true, false> walks every
+        segment exactly, the 4-wave build reads the table from global memory) and 2,000 (map and
+        table in global memory)."""
+        import torch
+        wx, wy = loop_map(n, seed=n + waves)
+        m = ppamd.Map(wx, wy)
+        from oracle_lib import compare
+        S = 2000
+        sc_dev = ppamd.synth_device(m, S, seed=n + 17 * waves, device=0)
+        prm = ppamd.default_params(n_speeds=5, emit_paths=True)
+        r = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
+        with ppamd.debug(ppamd.DBG_PREP_GROUP, 1):
+            with ppamd.debug(ppamd.DBG_PREP_WAVES, waves):
+                ppamd.evaluate(m, sc_dev, prm, r, device=0)
+        torch.cuda.synchronize()
+        got = ppamd.result_to_numpy(r)
+        ref = oracle_lib.oracle_eval(oracle_lib.load_oracle(), wx, wy, ppamd.scenes_to_numpy(sc_dev), prm, info=False)
+        e = compare(got, ref)
+        assert e <= 1e-6, e
