@@ -137,3 +137,24 @@ def test_certified_runs_vs_oracle(env, waves):
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=False)
     e = oracle_lib.compare(got, ref)
     print(f"one-lane K1 at {waves} waves, {S} scenes (cars at perpendiculars): max |dxy| {e:.3e} m")
+
+
+def test_certified_runs_far_from_origin_vs_oracle(env):
+    """The certified approach test's error bound grows with the coordinates' magnitude: the highway
+    map moved by (+35,000, +35,000) m (lane centres up to ~3.8e4 m from the origin, inside the
+    fastm bound of 4e4 that the table needs), cars at lane-point perpendiculars, the one-lane K1
+    (LDS table): bit-identical with the oracle."""
+    wx = np.asarray(env["wx"]) + 35000.0
+    wy = np.asarray(env["wy"]) + 35000.0
+    m = ppamd.Map(wx, wy)
+    shifted = dict(env)
+    shifted.update({"m": m, "wx": wx, "wy": wy, "geo": m.geometry()})
+    S = 3000
+    sc = walk_scenes(shifted, S, 5151, edge=True)
+    d = to_dev(shifted, sc)
+    prm = ppamd.default_params(emit_paths=True)
+    with ppamd.debug(ppamd.DBG_PREP_GROUP, 1):
+        got = run_gpu(shifted, d, prm)
+    ref = oracle_lib.oracle_eval(env["olib"], wx, wy, sc, prm, info=False)
+    e = oracle_lib.compare(got, ref)
+    print(f"map at +35 km, {S} scenes (cars at perpendiculars): max |dxy| {e:.3e} m")
