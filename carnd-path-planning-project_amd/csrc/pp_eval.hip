@@ -3522,10 +3522,11 @@ int split_parts(int64_t S) {
     return S > 393216 ? 3 : 2;
 }
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
-// 4 better. A round of 3 waves per SIMD takes ~0.188 ms, one of 4 ~0.286 ms (1 x MI355X, config-5
-// scenes: 2.07 ms for 32,768 waves at 3, 2.29 ms at 4); 262,144 scenes (BASELINE config 5 over 8
-// GPUs) = 4,096 waves = 1.33 rounds at 3 (0.352 ms measured) or exactly 1 at 4. PP_DBG_PREP_WAVES
-// forces 3 or 4.
+// 4 better. Round 5 (the approach table in the 3-wave build's LDS): a round of 3 waves per SIMD
+// takes ~0.150 ms (config 5: 1.65 ms for 32,768 waves = 11 rounds), one of 4 ~0.357 ms (spills,
+// the table in global memory); 262,144 scenes = 4,096 waves: 0.297 ms at 3, 0.357 at 4
+// (profiles/r05_ablations.txt), so the 4-wave build no longer wins at any size (round 4: 0.188 /
+// 0.286 ms per round, 4 waves at 262,144). PP_DBG_PREP_WAVES forces 3 or 4.
 int cu_count(int device) {
     static int cus[kMaxDev] = {};
     if (device < 0 || device >= kMaxDev) return 256;
@@ -3551,7 +3552,7 @@ bool prep_w4(int64_t Sv, int device) {
     if (f == 3 || f == 4) return f == 4;
     const int64_t waves = (Sv + 63) / 64, simds = 4LL * cu_count(device);
     const int64_t r3 = (waves + 3 * simds - 1) / (3 * simds), r4 = (waves + 4 * simds - 1) / (4 * simds);
-    return 286 * r4 < 188 * r3;
+    return 357 * r4 < 150 * r3;
 }
 // k_emit: batches up to this many scenes take the small-batch instantiation
 constexpr int64_t kEmitSmall = 65536;
