@@ -142,20 +142,21 @@ def shard_projection(t_full, t_shards):
             for n, t in sorted(t_shards.items())}
 
 
-def pmc_tag(S, Cn, N, emit_paths, D):
-    return f"k_cand_S{S}_C{Cn}_N{N}" + ("_paths" if emit_paths else "") + (f"_D{D}" if D > 1 else "")
+def pmc_tag(S, Cn, N, emit_paths, D, comfort=False):
+    return (f"k_cand_S{S}_C{Cn}_N{N}" + ("_paths" if emit_paths else "") + (f"_D{D}" if D > 1 else "")
+            + ("_comfort" if comfort else ""))
 
 
-def pmc_for(pmc_all, S, Cn, N, emit_paths, D):
+def pmc_for(pmc_all, S, Cn, N, emit_paths, D, comfort=False):
     """The PMC entry of this launch shape: the exact tag, else the largest profiled launch with the
     same candidates per scene, horizon, paths mode and draws (counter bytes and instructions per
     candidate carry over between batch sizes of one shape). Entries must state their launch size
     (candidates_per_launch): a counter total is meaningless without it."""
-    exact = pmc_all.get(pmc_tag(S, Cn, N, emit_paths, D))
+    exact = pmc_all.get(pmc_tag(S, Cn, N, emit_paths, D, comfort))
     cands = [exact] if exact else [
         e for e in pmc_all.values()
-        if (e.get("candidates_per_scene"), e.get("n_points"), e.get("emit_paths"), e.get("draws", 1)) ==
-        (Cn, N, bool(emit_paths), D)]
+        if (e.get("candidates_per_scene"), e.get("n_points"), e.get("emit_paths"), e.get("draws", 1),
+            bool(e.get("comfort"))) == (Cn, N, bool(emit_paths), D, bool(comfort))]
     if not cands:
         return None
     e = max(cands, key=lambda e: e.get("candidates_per_launch") or 0)
@@ -231,6 +232,8 @@ def parse(argv=None):
     ap.add_argument("--debug", action="append", default=[], metavar="KEY=VALUE",
                     help="library debug switch for A/B runs (include/pp.h PP_DBG_*): prep_group=G, "
                          "prep_waves=3|4, shape=1|2|3, split=1|2; recorded in config.debug, which marks the line not reportable")
+    ap.add_argument("--no-comfort", action="store_true",
+                    help="skip the comfort-mode (data-dependent argmin) side measurement of config 5 (1 GPU)")
     ap.add_argument("--no-shard-projection", action="store_true",
                     help="skip timing config 5's 2-, 4- and 8-GPU shards after the headline (1 GPU, config 5)")
     ap.add_argument("--cpu-ranks", action="store_true",
@@ -524,13 +527,14 @@ def main(argv=None):
     sp = stream.cuda_stream
     frames = max(a.rollout, 1)
 
-    def measure(first, S, steps, warmup):
+    def measure(first, S, steps, warmup, cost_mode=None):
         """One timed run over this rank's shard: W untimed steps, then K steps bracketed by a
         barrier + device synchronisation on both sides; returns (max-over-ranks seconds, per-kernel
         ms and launches of this rank, the resident scenes)."""
         m.reserve(local, S * D)
         p = ppamd.default_params(n_speeds=a.n_speeds, n_points=a.n_points,
-                                 cost_mode=prm.cost_mode, emit_paths=a.emit_paths, n_draws=a.draws,
+                                 cost_mode=prm.cost_mode if cost_mode is None else cost_mode,
+                                 emit_paths=a.emit_paths, n_draws=a.draws,
                                  noise_first_scene=first,
                                  speed_offsets=[-6, -4, -3, -2, -1, 0, 2] if a.n_speeds == 8 else None)
         traffic = None
@@ -634,10 +638,10 @@ def main(argv=None):
     k2_per_step = max(launches[1] // max(a.steps * frames, 1), 1)
     cands_launch = S * Cn // k2_per_step
     achieved = bpc * cands_launch / (k_cand_ms * 1e-3) / 1e9
-    pmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D)
+    pmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D, a.comfort)
     # the same fraction from the profiler's average K2 duration of this exact launch shape (a
     # committed rocprofv3 run of this command; durations do not carry over between batch sizes)
-    rp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D))
+    rp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D, a.comfort))
     rp = rp if rp and rp.get("launches_per_step") == k2_per_step and not a.rollout else None
     # counters and profiler durations of another library build describe another binary: dropped
     pmc, rp, stamp = profile_entries(pmc, rp, ppamd.lib_sha256())
@@ -726,6 +730,38 @@ def main(argv=None):
         out["shard_projection"] = dict(shard_projection(elapsed / a.steps, t_sh), what=(
             "config 5 on N GPUs = N independent shards of 2,097,152 / N scenes (no collective): speed-up "
             "t(full batch) / t(shard), both timed in this run (same protocol, steps and warmup)"))
+    if (world == 1 and a.scaling == "strong" and wname == "BASELINE config 5" and S == CONFIG5_SCENES
+            and not a.debug and not a.comfort and not a.no_comfort):
+        # the data-dependent decision (north_star's "argmin per scene") on the same batch: the
+        # comfort cost mode, where k_cand takes each scene's first-minimum cost and stores the
+        # winner's spline, and k_winner_st re-runs the winner with outputs
+        del scenes
+        torch.cuda.empty_cache()
+        cel, (cms, clh, cms_all, cla), scenes = measure(first, S, a.steps, a.warmup, ppamd.COST_COMFORT)
+        ck = {"k_prep": cms_all[0] / cla[0] if cla[0] else None, "k_cand": cms[1] / max(clh[1], 1),
+              "k_winner": cms_all[2] / cla[2] if cla[2] else None}
+        cstep = cel / a.steps * 1e3
+        cach = bpc * cands_launch / (ck["k_cand"] * 1e-3) / 1e9
+        cpmc = pmc_for(load_pmc_all(), S, Cn, a.n_points, a.emit_paths, D, True)
+        crp = load_rocprof_all().get(pmc_tag(S, Cn, a.n_points, a.emit_paths, D, True))
+        crp = crp if crp and crp.get("launches_per_step") == 1 else None
+        cpmc, crp, cstamp = profile_entries(cpmc, crp, ppamd.lib_sha256())
+        ctraffic, cpipe = roofline_fields(cpmc, cands_launch, bpc, ck["k_cand"])
+        out["comfort"] = {
+            "value": total_scenes * Cn * a.steps / cel, "unit": "candidate trajectories/s",
+            "ms_per_step": cstep, "kernels_ms_avg": ck,
+            "k_winner_share_of_step": (ck["k_winner"] / cstep) if ck["k_winner"] else None,
+            "roofline": {"bound": "hbm", "achieved": cach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": cach / HBM_PEAK_GBS, "kernel": "k_cand", "kernel_ms": ck["k_cand"],
+                         "algorithmic_bytes_per_candidate": bpc, "traffic": ctraffic, "traffic_pipeline": cpipe,
+                         "profile_stamp": cstamp,
+                         "frac_rocprof": (bpc * cands_launch / (crp["dominant_ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                          if crp else None),
+                         "kernel_ms_rocprof": crp["dominant_ms_per_launch"] if crp else None},
+            "what": ("BASELINE config 5's batch under the comfort cost (cost_mode 1): per scene the first "
+                     "minimum of the 15 candidate costs (k_cand, in LDS), the winner's spline slot stored, "
+                     "k_winner_st re-runs it with next_x/next_y; same timing protocol as the headline; "
+                     "k_prep and k_winner from the pass after the timed region")}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.rollout:
         model, nproc, share = host_cpu()
         threads = a.cpu_threads or share

@@ -31,10 +31,11 @@
 
 #include "../../include/pp.h"
 #include "pp_cartable.h"
-#ifdef PP_DIAG
-// diagnostic builds only (-DPP_DIAG): per event, [2k] lanes where it fired, [2k+1] waves where any
-// lane fired (the wave executes the branch). Read with pp_diag_read.
-__device__ unsigned long long g_diag[64];
+#if defined(PP_DIAG) || defined(PP_LIMCENSUS)
+// diagnostic builds only (-DPP_DIAG, -DPP_LIMCENSUS): per event, [2k] lanes where it fired,
+// [2k+1] waves where any lane fired (the wave executes the branch). Read with pp_diag_read.
+constexpr int kDiagWords = 96;
+__device__ unsigned long long g_diag[kDiagWords];
 __device__ __forceinline__ void diag(int k, bool c) {
     const unsigned long long b = __ballot(c);
     if (b && __lane_id() == (unsigned)__builtin_ctzll(__ballot(1))) {
@@ -42,9 +43,22 @@ __device__ __forceinline__ void diag(int k, bool c) {
         atomicAdd(&g_diag[2 * k + 1], 1ull);
     }
 }
+#endif
+#ifdef PP_DIAG
 #define PP_DIAGC(k, c) diag(k, c)
 #else
 #define PP_DIAGC(k, c) ((void)0)
+#endif
+// The limiter census (-DPP_LIMCENSUS; VERDICT r5 item 2, tests/test_full_batch.py): at every
+// decision of the acceleration limiter (src/main.cpp:941 and :972) the census build also evaluates
+// the reference's own operation sequence from the same state — the speed ramp's IEEE division,
+// glibc's atan2 of the step (pp_glibcm.h, bit for bit) and the wrapped difference of absolute
+// angles — and counts decisions within a relative 1e-12 of maximum_acc and decisions the two
+// sequences take differently (g_diag events 26-33, names in tests/test_full_batch.py).
+#ifdef PP_LIMCENSUS
+#define PP_CEN(k, c) diag(k, c)
+#else
+#define PP_CEN(k, c) ((void)0)
 #endif
 #ifdef PP_CENSUS
 // census builds only (-DPP_CENSUS): an assembly comment ";@R <output mode> <region>" at the start of
@@ -1686,6 +1700,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
     double rtt = ppm::rcp_nr(sc.ttime);
 #endif
     PP_DIAGC(20, true);     // (waves entering the loop)
+#ifdef PP_LIMCENSUS
+    double ref_pa = 0;      // the reference's prev_angle (src/main.cpp:906): the previous step's atan2
+#endif
     // the divisions by 50 and by the ramp time: reciprocal + correction (k_cand<false>: unchecked)
 #define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div50_nc(v))
     while (arg < 50 && ng < room) {
@@ -1780,6 +1797,29 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
         PP_REGION("acc");
         const double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
+#ifdef PP_LIMCENSUS
+        bool cen_r1, cen_r2;
+        {
+            const double spd_r = sc_get_speed(sc, cur_t);                 // :919 (IEEE division)
+            const double ast_r = ppg::atan2(y - pos_y, x - pos_x);        // :933
+            const double adf_r = ppm::fmod_2pi(ast_r - ref_pa + 3 * kPi) - kPi;   // :934
+            const double acc_r = fabs(spd_r - prev_speed) * 50, cacc_r = spd_r * 50 * fabs(adf_r);
+            const double mx = P.maximum_acc, tol = 1e-12 * fabs(mx);
+            cen_r1 = acc_r + cacc_r > mx;                                 // :941
+            cen_r2 = cen_r1;
+            if (cen_r1 && spd_r > prev_speed) {                           // :945-971, then :972
+                double na_r = mx - cacc_r;
+                if (na_r < 0) na_r = 0;
+                cen_r2 = na_r + cacc_r > mx;
+            }
+            PP_CEN(26, fabs(acc + cacc - mx) <= tol);
+            PP_CEN(27, fabs(acc_r + cacc_r - mx) <= tol);
+            PP_CEN(28, (acc + cacc > mx) != cen_r1);
+            PP_CEN(32, __double_as_longlong(cacc) != __double_as_longlong(cacc_r));
+            PP_CEN(33, __double_as_longlong(speed) != __double_as_longlong(spd_r));
+            ref_pa = ast_r;
+        }
+#endif
         PP_DIAGC(4, acc + cacc > P.maximum_acc);
         PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
         PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
@@ -1802,6 +1842,9 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 R.flags |= PP_ST_ACC_OVERRIDE;
             }
             PP_DIAGC(6, acc + cacc > P.maximum_acc);
+            PP_CEN(29, true);
+            PP_CEN(30, fabs(acc + cacc - P.maximum_acc) <= 1e-12 * fabs(P.maximum_acc));
+            PP_CEN(31, cen_r1 && (acc + cacc > P.maximum_acc) != cen_r2);
             PP_REGION("lim2");
             if (acc + cacc > P.maximum_acc) {                           // :972-1018
                 PP_REGION("adj");
@@ -1992,10 +2035,18 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 // single-frame and small-batch step, whose time is the winners' serial chain)
 // kPreA: the block's (single) scene has its fast-path spline slots built already (k_plan_frame's
 // second wave builds them while the first runs K1): phase A is skipped
+#ifndef PP_WSLOT
+#define PP_WSLOT 1            // 0: k_winner makes the decision and builds the winner's spline (A/B)
+#endif
+// k_winner's blocks and spline slots (kWinKnots = 9 previous + 6 control points, the real maximum)
+constexpr int kWinBlock = 64;
+constexpr int kWinKnots = 15;
+static_assert(PP_PREV_KEEP - 1 + 6 <= kWinKnots && kWinKnots <= kKP, "slot too small");
 template <bool kSlow, int kMode, int kEmitIn = 0, bool kPreA = false>
 __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
                                            const PrepV& pv, const pp_result& out, int SPB, int BPS,
-                                           double* rec, uint64_t* adjm, int64_t g, double* sm) {
+                                           double* rec, uint64_t* adjm, int64_t g, double* sm,
+                                           double* wslot = nullptr) {
     constexpr bool emit_in = kEmitIn == 1 && kMode == 1;
     constexpr bool win_inline = kEmitIn == 2 && kMode == 1;
     const int NS = P.n_speeds, Cv = NL * NS, N = P.n_points;
@@ -2034,6 +2085,8 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
     // kMode 1 with emit_in: each winner's step count and adjusted-step masks for the in-block K4
     uint64_t* sAdj = (uint64_t*)(((uintptr_t)(sSlow + SPB) + 7) & ~(uintptr_t)7);
     int* sNg = (int*)(sAdj + 2 * SPB);
+    // comfort mode with a stored winner slot: each lane's cost (the host sizes the LDS for it)
+    double* sCost = (double*)(((uintptr_t)(sNg + SPB) + 7) & ~(uintptr_t)7);
     if (tid < SPB) { sFlags[tid] = 0; sSlow[tid] = 0; }
 #ifdef PP_TRACE
     if (!kSlow && tid == 0) {
@@ -2246,6 +2299,7 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         const double cost = cand_cost(P, R, K, pv.score[L * Sv + v], L, T, vt, pv.open_mask[v],
                                       pv.ego_lane[v], flags);
         if (PP_CHKP(out.cost + s * C + c, cost, ncost, 14)) out.cost[s * C + c] = cost;
+        if (kMode == 0 && wslot && BPS == 1 && D == 1) sCost[tid] = cost;     // (k_winner_st's decision)
         if (D > 1) flags |= (uint32_t)pv.status[v];     // every draw's planner flags
         atomicOr(&sFlags[sc_l], flags);
     }
@@ -2257,6 +2311,40 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
         else atomicOr(&out.status[s0 + tid], st);     // zeroed by k_prep
     }
     if (!kSlow && tid == 0) PP_TRACE_AT(blockIdx.x, 6);
+    if (kMode == 0 && wslot && BPS == 1 && D == 1) {
+        // comfort mode (every candidate of the block's scenes in this block, no draws): the
+        // per-scene decision, k_winner's rule (first minimum over (lane, speed)) over the costs the
+        // lanes left in LDS, then the winner's spline slot copied from LDS to the stored-slot buffer,
+        // so k_winner_st re-runs the winner without building its spline a second time (the slot is
+        // what setup_lane builds, element for element)
+        int* sBest = sNg;
+        if (tid < nsc && ((sSlow[tid] != 0) == kSlow)) {
+            int best = 0;
+            double bc = 0;
+            for (int cc = 0; cc < Cv; cc++) {
+                const double cst = sCost[tid * C + cc];
+                if (cc == 0 || cst < bc) { bc = cst; best = cc; }
+            }
+            sBest[tid] = best;
+            out.winner[s0 + tid] = best;
+        }
+        __syncthreads();
+        constexpr int kItems = 5 * kWinKnots + 4;      // x, y, a, b, c of each knot, then the meta
+        // item-major: a wave's lanes store consecutive scenes of one item (one row of the buffer)
+        for (int idx = tid; idx < nsc * kItems; idx += (int)blockDim.x) {
+            const int e = idx / nsc, w = idx - e * nsc;
+            if ((sSlow[w] != 0) != kSlow) continue;
+            const int64_t s = s0 + w;
+            const Slot sl = lds_slot(sX, nslot, sMeta, w * NL + sBest[w] / NS);
+            if (e < 5 * kWinKnots) {
+                const int f = e / kWinKnots, i = e - f * kWinKnots;
+                const double val = f == 0 ? sl.x(i) : f == 1 ? sl.y(i) : f == 2 ? sl.a(i) : f == 3 ? sl.b(i) : sl.c(i);
+                wslot[(int64_t)e * S + s] = val;
+            } else {
+                ((int*)(wslot + (int64_t)5 * kWinKnots * S))[(int64_t)(e - 5 * kWinKnots) * S + s] = sl.m(e - 5 * kWinKnots);
+            }
+        }
+    }
     if (kMode == 1 && emit_in) {
         // K4 in the block (reference mode): the spline slots are free now, so the team computes
         // the sin/cos of every recorded turn of the block's winners into them (one item per
@@ -2296,10 +2384,10 @@ template <bool kSlow, int kMode>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 ? PP_CAND_WAVES2 : kCandWaves))) void k_cand(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_result out, int SPB, int BPS, double* rec, uint64_t* adjm,
                                               uint32_t* gbits, int64_t ngroups, const uint32_t* glist,
-                                              const uint32_t* gcount, int64_t g0) {
+                                              const uint32_t* gcount, int64_t g0, double* wslot) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     if (!kSlow) {
-        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g0 + blockIdx.x, sm);
+        cand_group<false, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g0 + blockIdx.x, sm, wslot);
         return;
     }
     // the flagged groups k_prep listed (each listed once: the first setter of its bit appends it)
@@ -2308,7 +2396,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 
         const int64_t g = glist[i];
         if (!PP_CHK(g < ngroups, 21, g)) continue;               // (never: k_prep lists this call's groups)
         __syncthreads();                                          // the previous group's LDS readers are done
-        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm);
+        cand_group<true, kMode>(mg, in, P, pv, out, SPB, BPS, rec, adjm, g, sm, wslot);
         if (threadIdx.x == 0) atomicAnd(&gbits[g >> 5], ~(1u << (g & 31)));
     }
 }
@@ -2322,40 +2410,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kMode == 2 
 // the loop rarely reads it. next_x/next_y are point-major ([i * S + s], the batch's own
 // convention): every step of the wave stores 512 contiguous bytes.
 // ------------------------------------------------------------------------------------------------
-constexpr int kWinBlock = 64;
-constexpr int kWinKnots = 15;
-static_assert(PP_PREV_KEEP - 1 + 6 <= kWinKnots, "slot too small");
+// the winner's re-run with outputs (best: its candidate index; sl: its spline slot, built)
 template <bool kSlow>
-__global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in, pp_params P,
-                                                      PrepV pv, pp_result out) {
-    __shared__ __attribute__((aligned(16))) double wsm[5 * kWinKnots * kWinBlock];
-    __shared__ int wmeta[4 * kWinBlock];
-    const MapV m = map_view(mg.buf, mg.n);
+__device__ __forceinline__ void winner_run(const pp_scene_batch& in, const pp_params& P, const PrepV& pv,
+                                           const pp_result& out, int64_t s, int64_t v0, int64_t Sv,
+                                           int best, const Slot& sl) {
     const int64_t S = in.n_scenes;
-    const int D = P.n_draws > 1 ? P.n_draws : 1;
-    const int64_t Sv = S * D;
-    const int j = threadIdx.x;
-    const int64_t s = (int64_t)blockIdx.x * kWinBlock + j;
-    const int64_t v0 = s * D;                 // the nominal (draw 0) prep record
-    if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
-    const int NS = P.n_speeds, Cv = NL * NS, C = D * Cv, N = P.n_points;
-    // decision: first minimum over (lane, k) of the cost averaged over the draws (summed in draw
-    // order, then / D; D = 1: the plain cost)
-    int best = 0;
-    double bc = 0;
-    for (int c = 0; c < Cv; c++) {
-        double sum = out.cost[s * C + c];
-        for (int d = 1; d < D; d++) sum += out.cost[s * C + d * Cv + c];
-        const double mean = sum / D;
-        if (out.draw_mean_cost) out.draw_mean_cost[s * Cv + c] = mean;
-        if (c == 0 || mean < bc) { bc = mean; best = c; }
-    }
+    const int NS = P.n_speeds, N = P.n_points;
     const int L = best / NS, k = best - L * NS;
-    // slot arrays interleaved by lane ([knot][lane]) so the 64 lanes' accesses spread over banks
-    const Slot sl = {wsm + j, wsm + kWinKnots * kWinBlock + j, wsm + 2 * kWinKnots * kWinBlock + j,
-                     wsm + 3 * kWinKnots * kWinBlock + j, wsm + 4 * kWinKnots * kWinBlock + j,
-                     wmeta + j, kWinBlock, kWinBlock};
-    setup_lane(m, P, in, pv, s, v0, Sv, L, sl);
     const double v = cand_speed(P, pv.ego_speed[v0], k);
     const SC sc = make_sc(P, pv, Sv, v0, L, v);
     const int K = pv.K[v0];
@@ -2370,6 +2432,58 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     for (int i = K + R.ng; i < N; i++) { out.next_x[(int64_t)i * S + s] = 0; out.next_y[(int64_t)i * S + s] = 0; }
     out.n_out[s] = K + R.ng;
     out.winner[s] = best;
+}
+
+template <bool kSlow>
+__global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in, pp_params P,
+                                                      PrepV pv, pp_result out) {
+    __shared__ __attribute__((aligned(16))) double wsm[5 * kWinKnots * kWinBlock];
+    __shared__ int wmeta[4 * kWinBlock];
+    const MapV m = map_view(mg.buf, mg.n);
+    const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
+    const int j = threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * kWinBlock + j;
+    const int64_t v0 = s * D;                 // the nominal (draw 0) prep record
+    if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
+    const int NS = P.n_speeds, Cv = NL * NS, C = D * Cv;
+    // decision: first minimum over (lane, k) of the cost averaged over the draws (summed in draw
+    // order, then / D; D = 1: the plain cost)
+    int best = 0;
+    double bc = 0;
+    for (int c = 0; c < Cv; c++) {
+        double sum = out.cost[s * C + c];
+        for (int d = 1; d < D; d++) sum += out.cost[s * C + d * Cv + c];
+        const double mean = sum / D;
+        if (out.draw_mean_cost) out.draw_mean_cost[s * Cv + c] = mean;
+        if (c == 0 || mean < bc) { bc = mean; best = c; }
+    }
+    // slot arrays interleaved by lane ([knot][lane]) so the 64 lanes' accesses spread over banks
+    const Slot sl = {wsm + j, wsm + kWinKnots * kWinBlock + j, wsm + 2 * kWinKnots * kWinBlock + j,
+                     wsm + 3 * kWinKnots * kWinBlock + j, wsm + 4 * kWinKnots * kWinBlock + j,
+                     wmeta + j, kWinBlock, kWinBlock};
+    setup_lane(m, P, in, pv, s, v0, Sv, best / NS, sl);
+    winner_run<kSlow>(in, P, pv, out, s, v0, Sv, best, sl);
+}
+
+// Round 6: k_cand made the decision (out.winner) and stored the winner's spline slot
+// ([field * kWinKnots + knot][S] doubles, then the 4 meta ints [k][S]): no argmin, no spline build
+// and no LDS here, so the block is 256 lanes and occupancy is the registers' (k_winner holds 38 KB
+// of LDS per 64 lanes: one wave per SIMD).
+template <bool kSlow>
+__global__ __launch_bounds__(256) void k_winner_st(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
+                                                   const double* wslot) {
+    const int64_t S = in.n_scenes;
+    const int D = P.n_draws > 1 ? P.n_draws : 1;
+    const int64_t Sv = S * D;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t v0 = s * D;
+    if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
+    double* b = const_cast<double*>(wslot) + s;
+    const int64_t F = (int64_t)kWinKnots * S;
+    const Slot sl = {b, b + F, b + 2 * F, b + 3 * F, b + 4 * F, (int*)(const_cast<double*>(wslot) + 5 * F) + s, S, S};
+    winner_run<kSlow>(in, P, pv, out, s, v0, Sv, out.winner[s], sl);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3108,6 +3222,9 @@ constexpr int kPrepI = 7;
 // only after that stream has drained (it is the only stream using it).
 // the split of shard-sized batches: parts (streams) per call, at most kSplitMax (split_parts)
 constexpr int kSplitMax = 4;
+// parts per call: a batch beyond kSplitMaxScenes runs as chunks of parts, part t on stream t % streams
+// (split_chunks); each part has its own flagged-group count word and 4 timing-event slots
+constexpr int kPartMax = 16;
 #ifndef PP_SPLIT_PARTS
 #define PP_SPLIT_PARTS 0      // 0: by batch size (split_parts); 2..4 forced (A/B builds)
 #endif
@@ -3142,7 +3259,7 @@ struct DevState {
     pptab::CarTable plan_table;   // pp_plan_frame's persistent car table (the reference's std::map)
     int timing = 0;               // pp_timing_enable: 0 off, 1 every kernel, 2 K2 only
     std::vector<hipEvent_t> ev_pool;
-    // groups of 4 kSplitMax per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch
+    // groups of 4 kPartMax per pp_eval: before K1, after K1, after K2, after K3/K4 on the launch
     // stream (the split: those four per part, each part's on its own stream, events 4 h .. 4 h + 3)
     std::vector<hipEvent_t> ev_rec;
     // per group: bit 0 K3/K4 launched, bits 1-3 the split's parts (0: none), bit 4 K2's events only,
@@ -3205,6 +3322,7 @@ void fill_ptab(pp_map* M) {
 // hold 1-4); a cell with more, or away from the road, has none (0xFFFFFFFF: the kernel scans).
 // Maps of more than 65,535 waypoints, or whose table would take more than 5e7 distance tests to
 // build, get no table.
+constexpr double kWgridMaxCells = 4e6;
 void build_wgrid(pp_map* M) {
     constexpr double kCell = 16.0, kNear = 32.0, kGrow = 0.5;
     const int n = M->n;
@@ -3222,6 +3340,9 @@ void build_wgrid(pp_map* M) {
     const double wdt = x1 - x0 + 4 * kNear, hgt = y1 - y0 + 4 * kNear;
     if (!(wdt / kCell < 1e5 && hgt / kCell < 1e5)) return;
     const int gnx = (int)std::ceil(wdt / kCell), gny = (int)std::ceil(hgt / kCell);
+    // at most 4e6 cells (a 32 km square; 32 MB on the host and the device): a map spread wider
+    // keeps the full scan (two waypoints 1,000 km apart would ask for ~4e9 cells)
+    if ((double)gnx * (double)gny > kWgridMaxCells) return;
     // cells near the polyline: sample every segment every 2 m, mark cells within kNear
     std::vector<uint8_t> near((size_t)gnx * gny, 0);
     const int R = (int)std::ceil(kNear / kCell);
@@ -3324,6 +3445,15 @@ void build_atab(pp_map* M) {
     M->atab.swap(t);
 }
 
+// The optional per-map tables (cell table, segment reciprocals, approach table) speed K1 up and
+// never change a result: a map whose tables cannot be built (an allocation failure included) runs
+// without them. Nothing here throws across the C-ABI.
+void build_tables(pp_map* M) {
+    try { build_wgrid(M); } catch (...) { M->wgrid.clear(); M->wgrid.shrink_to_fit(); M->wg = WGrid{}; }
+    try { build_wseg(M); } catch (...) { M->wseg.clear(); M->wseg.shrink_to_fit(); }
+    try { build_atab(M); } catch (...) { M->atab.clear(); M->atab.shrink_to_fit(); }
+}
+
 void free_map_tables(DevState& D) {
     if (D.wgrid) (void)hipFree(D.wgrid);
     if (D.wseg) (void)hipFree(D.wseg);
@@ -3396,9 +3526,7 @@ int build_map(pp_map* M, const double* wx, const double* wy, int n) {
         }
     }
     fill_ptab(M);
-    build_wgrid(M);
-    build_wseg(M);
-    build_atab(M);
+    build_tables(M);
     M->lanetab.assign(5 * NL * (size_t)n, 0.0);
     double* t = M->lanetab.data();
     for (int r = 0; r < NL; r++)
@@ -3509,10 +3637,16 @@ bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // or draws, one K1 lane per scene: more than 65,536 scenes, prep_group), 2 turns it off; the parts
 // of the last call are read back with PP_DBG_LAST_PARTS.
 constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 1572864;
+#ifndef PP_SPLIT_BIG
+#define PP_SPLIT_BIG 1        // 0: batches beyond kSplitMaxScenes run on one stream (A/B builds)
+#endif
+constexpr int64_t kChunkScenes = 1048576;
 bool split_on(int64_t S) {
     const int f = dbg(PP_DBG_SPLIT);
     if (f == 2) return false;
-    return f == 1 ? true : (S >= kSplitMin && S <= kSplitMaxScenes);
+    // forced: any batch of at least 2,048 scenes (its parts then never come out empty)
+    if (f == 1) return S >= 2048;
+    return S >= kSplitMin && (S <= kSplitMaxScenes || PP_SPLIT_BIG);
 }
 // parts of a split batch: 2 up to 393,216 scenes (BASELINE config 5's N = 8 shard, 262,144: 1.32 ms
 // against 1.35 / 1.37 ms with 3 / 4 parts), 3 beyond (its N = 4 shard, 524,288: 2.52 ms against
@@ -3520,6 +3654,17 @@ bool split_on(int64_t S) {
 int split_parts(int64_t S) {
     if (PP_SPLIT_PARTS >= 2 && PP_SPLIT_PARTS <= kSplitMax) return PP_SPLIT_PARTS;
     return S > 393216 ? 3 : 2;
+}
+// chunks of a split batch: a batch beyond kSplitMaxScenes runs as ceil(S / 1,048,576) sequential
+// chunks of split_parts parts each (chunk c + 1 starts when every part of chunk c has ended).
+// Round 6, BASELINE config 5 (2,097,152 scenes), same box, alternating (tools/chunk_probe.py,
+// profiles/r06_chunk_probe.txt): one stream 9.89-9.99 ms, the 3-part split 9.90-9.93, two 1 M
+// chunks of 3 parts 9.78-9.81, four 512 k chunks 9.93-9.94; 6 parts pipelined over the 3 streams
+// without the join between chunks 10.00-10.04.
+int split_chunks(int64_t S) {
+    if (S <= kSplitMaxScenes) return 1;
+    const int64_t c = (S + kChunkScenes - 1) / kChunkScenes;
+    return (int)std::min<int64_t>(c, kPartMax / kSplitMax);
 }
 // K1 (one lane per evaluation): 3 waves per SIMD, or 4 where the batch's waves fill whole rounds of
 // 4 better. Round 5 (the approach table in the 3-wave build's LDS): a round of 3 waves per SIMD
@@ -3614,7 +3759,7 @@ int ensure_gbits(StreamWS& W, hipStream_t st, int64_t ngroups) {
     if (W.gbits) { (void)hipStreamSynchronize(st); (void)hipFree(W.gbits); W.gbits = nullptr; W.gbits_cap = 0; }
     const int64_t cap = std::max<int64_t>(words, 1024);
     // [bits: cap words][flagged-group count][the split's second-half count][list: 32 cap entries]
-    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + kSplitMax + 32 * cap);
+    const size_t bytes = sizeof(uint32_t) * (size_t)(cap + kPartMax + 32 * cap);
     if (hipMalloc(&W.gbits, bytes) != hipSuccess) return PP_ERR_NOMEM;
     if (hipMemsetAsync(W.gbits, 0, bytes, st) != hipSuccess) return PP_ERR_HIP;
     W.gbits_cap = cap;
@@ -3743,11 +3888,11 @@ int32_t pp_trace_read(unsigned long long* out, int64_t words) {   // diagnostic 
     return 0;
 }
 #endif
-#ifdef PP_DIAG
-int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic builds only
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
+#if defined(PP_DIAG) || defined(PP_LIMCENSUS)
+int32_t pp_diag_read(unsigned long long* out, int32_t reset) {   // diagnostic builds only (96 words)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * kDiagWords) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[64] = {};
+        unsigned long long z[kDiagWords] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
@@ -3782,7 +3927,8 @@ int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** ou
     if (!wx || !wy || !out || n < 3 || n > kMaxWaypoints) return PP_ERR_ARG;
     pp_map* M = new (std::nothrow) pp_map();
     if (!M) return PP_ERR_NOMEM;
-    const int rc = build_map(M, wx, wy, n);
+    int rc;
+    try { rc = build_map(M, wx, wy, n); } catch (...) { rc = PP_ERR_NOMEM; }   // (host allocations)
     if (rc != PP_OK) { delete M; return rc; }
     *out = M;
     return PP_OK;
@@ -3790,8 +3936,14 @@ int32_t pp_map_create(const double* wx, const double* wy, int32_t n, pp_map** ou
 
 // Map::Init on the device from device waypoint arrays; the derived tables are mirrored to the host
 // (for pp_map_geometry, the host generator and other devices).
+static int32_t map_create_device(const double* d_wx, const double* d_wy, int32_t n, int32_t device,
+                                 void* hip_stream, pp_map** out);
 int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, int32_t device, void* hip_stream,
                              pp_map** out) {
+    try { return map_create_device(d_wx, d_wy, n, device, hip_stream, out); } catch (...) { return PP_ERR_NOMEM; }
+}
+static int32_t map_create_device(const double* d_wx, const double* d_wy, int32_t n, int32_t device,
+                                 void* hip_stream, pp_map** out) {
     if (!d_wx || !d_wy || !out || n < 3 || n > kMaxWaypoints || device < 0 || device >= kMaxDev) return PP_ERR_ARG;
     pp_map* M = new (std::nothrow) pp_map();
     if (!M) return PP_ERR_NOMEM;
@@ -3831,9 +3983,7 @@ int32_t pp_map_create_device(const double* d_wx, const double* d_wy, int32_t n, 
         return rc;
     }
     fill_ptab(M);
-    build_wgrid(M);
-    build_wseg(M);
-    build_atab(M);
+    build_tables(M);
     if (upload_wgrid(M, D) != PP_OK) {
         free_map_tables(D);
         (void)hipFree(D.map); (void)hipFree(D.lanetab);
@@ -3959,6 +4109,17 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         rec = rec_buf(W.rec);
         adjm = adj_buf(W.rec, W.rec_cap);
     }
+    // comfort mode and draws without paths, every scene's candidates in one block: k_cand makes the
+    // decision and stores the winner's spline slot in the record's memory (616 B per scene of its
+    // 3,088), k_winner_st re-runs the winner from it
+    double* wslot = nullptr;
+    size_t cand_lds = cg.lds;
+    if (PP_WSLOT && !ref_direct && !prm->emit_paths && cg.bps == 1 && Dn == 1) {
+        rc = ensure_rec(W, st, S);
+        if (rc) return rc;
+        wslot = rec_buf(W.rec);
+        cand_lds = ((cg.lds + 7) & ~(size_t)7) + sizeof(double) * 256;     // + sCost
+    }
     if (dbg(PP_DBG_POISON)) {
         // every call starts from NaN-filled (0xFF) intermediates and outputs, so no kernel can lean
         // on what an earlier call left there (or on an output element it never writes); the
@@ -3974,7 +4135,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             if (w) return PP_ERR_STATE;
         const bool ok = fill(W.ws, prep_bytes(W.ws_cap)) &&
                         fill(W.rec, W.rec ? rec_bytes(W.rec_cap) : 0) &&
-                        fill(W.gbits + W.gbits_cap + kSplitMax, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
+                        fill(W.gbits + W.gbits_cap + kPartMax, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
                         fill(out->winner, 4 * S) && fill(out->n_out, 4 * S) && fill(out->status, 4 * S) &&
                         fill(out->next_x, 8 * N * S) && fill(out->next_y, 8 * N * S) &&
                         fill(out->cost, 8 * Cn * S) && fill(out->info, sizeof(pp_scene_info) * S) &&
@@ -3995,13 +4156,13 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     // k_prep<true, false> stages the approach table after the map where both fit a block's 64 KB
     mg.atab_lds = DS.atab && sizeof(double) * (((kMapArrays * (size_t)M->n + 1) & ~(size_t)1) + kAtabD * (size_t)M->n) <= 65536;
     // tall: events at every kernel boundary; tk2: at K2's (PP_TIMING_K2 records only those two).
-    // The call's record is a group of 4 kSplitMax slots (before K1, after K1, after K2, after
+    // The call's record is a group of 4 kPartMax slots (before K1, after K1, after K2, after
     // K3/K4, per part); a slot takes an event from the pool when it is first recorded, so a
     // K2-only call takes 2 events (2 per part when split) and an all-kernel call 4 per part
     const bool timing = DS.timing != 0, tall = DS.timing == 1, tk2 = timing;
     const size_t ev_base = DS.ev_rec.size();
     if (timing) {
-        DS.ev_rec.resize(ev_base + 4 * kSplitMax, nullptr);
+        DS.ev_rec.resize(ev_base + 4 * kPartMax, nullptr);
         DS.ev_kind.push_back((!(ref_direct && prm->emit_paths) && !emit_in ? 1 : 0) | (tall ? 0 : 16));
     }
     auto ev = [&](int i) -> hipEvent_t {
@@ -4019,7 +4180,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     GroupBits gb = {};
     gb.bits = W.gbits; gb.SPB = cg.spb; gb.BPS = cg.bps; gb.C = Cn_;
     gb.count = W.gbits + W.gbits_cap;
-    gb.list = gb.count + kSplitMax;
+    gb.list = gb.count + kPartMax;
 #ifdef PP_CHECK
     {   // checking builds: the bounds of every buffer this call's kernels store into
         ChkLim L = {};
@@ -4059,65 +4220,75 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
-    if (hipMemsetAsync(gb.count, 0, kSplitMax * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
+    if (hipMemsetAsync(gb.count, 0, kPartMax * sizeof(uint32_t), st) != hipSuccess) return PP_ERR_HIP;
     const bool split = ref_direct && !P.emit_paths && !fused && cg.bps == 1 && Dn == 1 &&
                        prep_group(Sv) == 1 && split_on(S);
-    g_dbg[PP_DBG_LAST_PARTS].store(split ? split_parts(S) : 1, std::memory_order_relaxed);
+    g_dbg[PP_DBG_LAST_PARTS].store(1, std::memory_order_relaxed);
     if (split) {
-        // split_parts(S) parts at group boundaries: part h takes groups [G h / P, G (h + 1) / P) and
-        // their scenes, part 0 on the caller's stream, part h > 0 on stream st2[h - 1]; each part
-        // its own flagged-group list (count word h, its list from its first group's index on).
+        // NT = streams x chunks parts at group boundaries: part t takes groups [G t / NT, G (t + 1) /
+        // NT) and their scenes, on stream t % NS (stream 0: the caller's, else st2[.]); each part its
+        // own flagged-group list (count word t, its list from its first group's index on).
+        // Chunks run one after another (fork and join per chunk).
         // Timing: each part's kernels by events on its own stream; pp_timing_read counts each stage
-        // once per call, the span from the first part's start to the last part's end (the parts
-        // overlap, so one part's duration understates the stage's throughput).
-        const int NP = split_parts(S);
+        // once per call, as the span from a chunk's first part's start to its last part's end (the
+        // parts overlap, so one part's duration understates the stage's throughput), summed over
+        // the chunks.
+        const int NS = split_parts(S), NC = split_chunks(S), NT = NS * NC;
         if (!W.fork && hipEventCreateWithFlags(&W.fork, hipEventDisableTiming) != hipSuccess) return PP_ERR_HIP;
-        for (int k = 0; k < NP - 1; k++)
+        for (int k = 0; k < NS - 1; k++)
             if (!W.st2[k] && (hipStreamCreateWithFlags(&W.st2[k], hipStreamNonBlocking) != hipSuccess ||
                               hipEventCreateWithFlags(&W.join[k], hipEventDisableTiming) != hipSuccess))
                 return PP_ERR_HIP;
         const int64_t G = cg.groups;
-        if (timing) DS.ev_kind.back() |= NP << 1;
-        if (hipEventRecord(W.fork, st) != hipSuccess) return PP_ERR_HIP;
-        for (int k = 0; k < NP - 1; k++)
-            if (hipStreamWaitEvent(W.st2[k], W.fork, 0) != hipSuccess) return PP_ERR_HIP;
         const bool lmap = mg.n <= kLdsMapMax;
         const size_t lds = lmap ? sizeof(double) * kMapArrays * (size_t)mg.n : 0;
         const size_t lds_a = lmap && mg.atab_lds ? prep_lds_atab(mg.n) : lds;    // k_prep<true, false>
         MapG mga = mg;
         if (!mg.atab_lds) mga.atab = nullptr;
-        for (int h = 0; h < NP; h++) {
-            hipStream_t sh = h == 0 ? st : W.st2[h - 1];
-            const int64_t g0 = G * h / NP, g1 = G * (h + 1) / NP;
-            const int64_t v0 = std::min<int64_t>(S, g0 * cg.spb), v1 = std::min<int64_t>(S, g1 * cg.spb);
-            if (v1 <= v0) continue;     // (never: the split takes batches of >= 2,048 scenes)
-            GroupBits gbh = gb;
-            gbh.count = gb.count + h;
-            gbh.list = gb.list + g0;
-            const int eh = 4 * h;
-            if (tall) (void)hipEventRecord(ev(eh), sh);
-            const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
-            if (prep_w4(v1 - v0, device)) {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
-            } else {
-                if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1);
-                else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+        int launched = 0;     // parts launched (an empty part is skipped; never at >= 2,048 scenes)
+        for (int c = 0; c < NC; c++) {
+            // fork: the chunk's other streams start behind everything before it on the caller's stream
+            if (hipEventRecord(W.fork, st) != hipSuccess) return PP_ERR_HIP;
+            for (int k = 0; k < NS - 1; k++)
+                if (hipStreamWaitEvent(W.st2[k], W.fork, 0) != hipSuccess) return PP_ERR_HIP;
+            for (int h = 0; h < NS; h++) {
+                const int t = c * NS + h;
+                hipStream_t sh = h == 0 ? st : W.st2[h - 1];
+                const int64_t g0 = G * t / NT, g1 = G * (t + 1) / NT;
+                const int64_t v0 = std::min<int64_t>(S, g0 * cg.spb), v1 = std::min<int64_t>(S, g1 * cg.spb);
+                if (v1 <= v0) continue;
+                GroupBits gbh = gb;
+                gbh.count = gb.count + t;
+                gbh.list = gb.list + g0;
+                const int eh = 4 * launched++;
+                if (tall) (void)hipEventRecord(ev(eh), sh);
+                const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
+                if (prep_w4(v1 - v0, device)) {
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                } else {
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                }
+                if (tk2) (void)hipEventRecord(ev(eh + 1), sh);
+                const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
+                hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
+                                   cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0, (double*)nullptr);
+                hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
+                                   cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0, (double*)nullptr);
+                if (tk2) (void)hipEventRecord(ev(eh + 2), sh);
+                hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
+                                   rec, adjm, v0, v1);
+                if (tall) (void)hipEventRecord(ev(eh + 3), sh);
             }
-            if (tk2) (void)hipEventRecord(ev(eh + 1), sh);
-            const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
-            hipLaunchKernelGGL((k_cand<false, 1>), dim3((unsigned)(g1 - g0)), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
-                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
-            hipLaunchKernelGGL((k_cand<true, 1>), dim3(nsl), dim3(cg.threads), cg.lds, sh, mg, B, P, pv, R,
-                               cg.spb, cg.bps, rec, adjm, W.gbits, G, gbh.list, gbh.count, g0);
-            if (tk2) (void)hipEventRecord(ev(eh + 2), sh);
-            hipLaunchKernelGGL(k_emit<kEmitRows>, dim3((unsigned)((v1 - v0 + 255) / 256)), dim3(256), 0, sh, B, P, pv, R,
-                               rec, adjm, v0, v1);
-            if (tall) (void)hipEventRecord(ev(eh + 3), sh);
+            // join: the caller's stream waits for the chunk's other streams
+            for (int k = 0; k < NS - 1; k++)
+                if (hipEventRecord(W.join[k], W.st2[k]) != hipSuccess || hipStreamWaitEvent(st, W.join[k], 0) != hipSuccess)
+                    return PP_ERR_HIP;
         }
-        for (int k = 0; k < NP - 1; k++)
-            if (hipEventRecord(W.join[k], W.st2[k]) != hipSuccess || hipStreamWaitEvent(st, W.join[k], 0) != hipSuccess)
-                return PP_ERR_HIP;
+        // (the timing record: parts launched, and parts per chunk for the per-chunk spans)
+        if (timing) DS.ev_kind.back() |= (launched << 8) | (NC > 1 ? NS << 16 : 0);
+        g_dbg[PP_DBG_LAST_PARTS].store(launched, std::memory_order_relaxed);
         if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
         return PP_OK;
     }
@@ -4160,10 +4331,10 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         const int64_t ng = cg.groups;
         if (tk2) (void)hipEventRecord(ev(1), st);
 #define PP_LAUNCH_CAND(MODE)                                                                              \
-        hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0);          \
-        hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R, \
-                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0)
+        hipLaunchKernelGGL((k_cand<false, MODE>), dim3(nb), dim3(cg.threads), cand_lds, st, mg, B, P, pv, R, \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0, wslot);   \
+        hipLaunchKernelGGL((k_cand<true, MODE>), dim3(nslow), dim3(cg.threads), cand_lds, st, mg, B, P, pv, R, \
+                           cg.spb, cg.bps, rec, adjm, W.gbits, ng, gb.list, gb.count, (int64_t)0, wslot)
         if (P.emit_paths) { PP_LAUNCH_CAND(2); }
         else if (ref_direct && fused) {
             hipLaunchKernelGGL(k_cand_small, dim3(nb), dim3(cg.threads), cg.lds, st, mg, B, P, pv, R,
@@ -4187,8 +4358,14 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     // K3 (comfort mode, or any mode with draws): argmin + winner path
     if (!ref_direct) {
         const int64_t blocks = (S + kWinBlock - 1) / kWinBlock;
-        hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
-        hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+        if (wslot) {
+            const unsigned b256 = (unsigned)((S + 255) / 256);
+            hipLaunchKernelGGL((k_winner_st<false>), dim3(b256), dim3(256), 0, st, B, P, pv, R, (const double*)wslot);
+            hipLaunchKernelGGL((k_winner_st<true>), dim3(b256), dim3(256), 0, st, B, P, pv, R, (const double*)wslot);
+        } else {
+            hipLaunchKernelGGL((k_winner<false>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+            hipLaunchKernelGGL((k_winner<true>), dim3((unsigned)blocks), dim3(kWinBlock), 0, st, mg, B, P, pv, R);
+        }
     }
     if (tall) (void)hipEventRecord(ev(3), st);
     if (hipGetLastError() != hipSuccess) return PP_ERR_HIP;
@@ -4248,7 +4425,7 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
     DeviceGuard g(device);
     for (int k = 0; k < 3; k++) { ms3[k] = 0; launches3[k] = 0; }
     int rc = PP_OK;
-    constexpr int EG = 4 * kSplitMax;
+    constexpr int EG = 4 * kPartMax;
     const size_t ng = D.ev_rec.size() / EG;
     // signed milliseconds from a to b (either order)
     auto dt = [&](hipEvent_t a, hipEvent_t b, float& t) {
@@ -4259,26 +4436,32 @@ int32_t pp_timing_read(pp_map* M, int32_t device, double* ms3, int64_t* launches
         return false;
     };
     for (size_t i = 0; i < ng; i++) {
-        const int kind = D.ev_kind[i], parts = (kind >> 1) & 7, np = parts ? parts : 1;
+        const int kind = D.ev_kind[i], parts = (kind >> 8) & 0xFF, np = parts ? parts : 1;
+        const int per = (kind >> 16) & 0xF, pc = per ? per : np;    // parts per chunk
         const bool k2only = (kind & 16) != 0;
         hipEvent_t* e0 = &D.ev_rec[EG * i];
         for (int h = 0; h < np; h++) {
             hipEvent_t last = k2only ? e0[4 * h + 2] : e0[4 * h + 3];
             if (!last || hipEventSynchronize(last) != hipSuccess) rc = PP_ERR_HIP;
         }
-        // stage k (0: K1, 1: K2, 2: K3/K4) of a call: from its earliest start to its latest end over
-        // the parts (one stream: the kernel's own interval; a split call's parts overlap, and the
-        // stage's time is the span they cover together, as in a kernel trace), one launch per call
+        // stage k (0: K1, 1: K2, 2: K3/K4) of a call: per chunk, from its earliest start to its
+        // latest end over the chunk's parts (one stream: the kernel's own interval; a split call's
+        // parts overlap, and the stage's time is the span they cover together, as in a kernel
+        // trace), summed over the chunks; one launch per call
         for (int k = 0; k < 3; k++) {
             if (k != 1 && (k2only || (k == 0 && (kind & 32)) || (k == 2 && !(kind & 1)))) continue;
-            float lo = 0, hi = 0;
+            float sum = 0;
             bool ok = true;
-            for (int h = 0; h < np && ok; h++) {
-                float a, b;
-                ok = dt(e0[1], e0[4 * h + k], a) && dt(e0[1], e0[4 * h + k + 1], b);
-                if (ok) { lo = h == 0 ? a : std::min(lo, a); hi = h == 0 ? b : std::max(hi, b); }
+            for (int c0 = 0; c0 < np && ok; c0 += pc) {
+                float lo = 0, hi = 0;
+                for (int h = c0; h < std::min(np, c0 + pc) && ok; h++) {
+                    float a, b;
+                    ok = dt(e0[1], e0[4 * h + k], a) && dt(e0[1], e0[4 * h + k + 1], b);
+                    if (ok) { lo = h == c0 ? a : std::min(lo, a); hi = h == c0 ? b : std::max(hi, b); }
+                }
+                sum += hi - lo;
             }
-            if (ok) { ms3[k] += hi - lo; launches3[k]++; }
+            if (ok) { ms3[k] += sum; launches3[k]++; }
         }
         for (int k = 0; k < EG; k++)
             if (D.ev_rec[EG * i + k]) D.ev_pool.push_back(D.ev_rec[EG * i + k]);

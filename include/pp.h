@@ -385,10 +385,11 @@ int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
  *                      slow-group bitmap is all zero (PP_ERR_STATE otherwise), so no kernel can pass
  *                      a test on what an earlier call left behind
  *   PP_DBG_SPLIT       multi-stream split of reference-mode batches (2 or 3 parts, each K1 -> K2 ->
- *                      K4 on its own stream): 1 on for every batch the split can take (reference
- *                      mode without paths or draws, more than 65,536 scenes), 2 off (0: batches of
- *                      131,072 to 1,572,864 scenes)
- *   PP_DBG_LAST_PARTS  read-only: the streams (parts) the last pp_eval used, 1 when not split
+ *                      K4 on its own stream; beyond 1,572,864 scenes sequential chunks of ~1,048,576
+ *                      scenes, 3 parts each): 1 on for every batch the split can take (reference
+ *                      mode without paths or draws, more than 65,536 scenes, at least 2,048), 2 off
+ *                      (0: batches of 131,072 scenes and more)
+ *   PP_DBG_LAST_PARTS  read-only: the parts the last pp_eval launched, 1 when not split
  * Returns PP_ERR_ARG for an unknown key or value. */
 #define PP_DBG_PREP_GROUP  0
 #define PP_DBG_PREP_WAVES  1

@@ -30,6 +30,20 @@
 
 typedef struct { double x, y; } P2;
 
+/* Near-threshold census of the acceleration limiter's decisions (src/main.cpp:941, :972; test
+ * infrastructure for tests/test_full_batch.py): per calling thread, [0] / [1]
+ * decisions taken at :941 / :972, [2] / [3] those whose left side lies within a relative 1e-12 of
+ * maximum_acc. ppo_census reads (and optionally clears) the calling thread's counters. */
+static _Thread_local long long o_census[4];
+static inline void census(int which, double lhs, double mx) {
+    o_census[which]++;
+    if (fabs(lhs - mx) <= 1e-12 * fabs(mx)) o_census[2 + which]++;
+}
+void ppo_census(long long* out4, int reset) {
+    memcpy(out4, o_census, sizeof o_census);
+    if (reset) memset(o_census, 0, sizeof o_census);
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* helpers.h geometry                                                                          */
 /* ------------------------------------------------------------------------------------------ */
@@ -845,6 +859,7 @@ static int build_traj(const OMap* m, const pp_params* P, const OPrep* pr, int L,
         double adiff = fmod(astep - prev_angle + 3 * O_PI, 2 * O_PI) - O_PI;
         double cacc = speed * 50 * fabs(adiff);
         double eff_c = cacc;
+        census(0, acc + cacc, P->maximum_acc);
         if (acc + cacc > P->maximum_acc) {
             if (speed > prev_speed) {
                 double na = P->maximum_acc - cacc;
@@ -857,6 +872,7 @@ static int build_traj(const OMap* m, const pp_params* P, const OPrep* pr, int L,
                 acc = na;
                 st->override_hit = 1;
             }
+            census(1, acc + cacc, P->maximum_acc);
             if (acc + cacc > P->maximum_acc) {
                 double nc = P->maximum_acc - acc;
                 if (nc < 0) nc = 0;

@@ -1,6 +1,6 @@
 """The multi-stream split (pp_eval, include/pp.h PP_DBG_SPLIT): reference-mode batches of about a
 2-, 4- or 8-GPU shard's size run as 2 parts (up to 393,216 scenes) or 3 parts, each K1 -> K2 -> K4 on
-its own stream. The parts write disjoint ranges of every buffer and keep separate flagged-group
+its own stream; larger batches (round 6) as sequential chunks of about 1,048,576 scenes, 3 parts each. The parts write disjoint ranges of every buffer and keep separate flagged-group
 lists, so the results must be the one-stream launch's BIT FOR BIT, including the scenes routed to
 k_cand<true> and part boundaries that split no group; a sample is checked against the oracle."""
 import numpy as np
@@ -20,12 +20,15 @@ def env():
             "olib": oracle_lib.load_oracle(), "dev": torch.device("cuda", 0)}
 
 
-def run(env, sc, prm, mode):
+def run(env, sc, prm, mode, group=0):
     t = env["torch"]
     S = sc["ego_x"].shape[0]
     d = {k: t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
     r = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"])
-    with ppamd.debug(ppamd.DBG_SPLIT, mode):
+    # (a forced K1 group of 1 also forces the three-kernel shape: small batches run one fused launch)
+    shape = ppamd.SHAPE_SPLIT if group == 1 else ppamd.SHAPE_AUTO
+    with ppamd.debug(ppamd.DBG_SPLIT, mode), ppamd.debug(ppamd.DBG_PREP_GROUP, group), \
+            ppamd.debug(ppamd.DBG_SHAPE, shape):
         ppamd.evaluate(env["m"], d, prm, r, device=0)
     t.cuda.synchronize()
     return ppamd.result_to_numpy(r)
@@ -33,25 +36,39 @@ def run(env, sc, prm, mode):
 
 # (S, mode, parts): the automatic split (131,072 to 1,572,864 scenes) and the forced one below its
 # range (more than 65,536 scenes: one K1 lane per scene); 70,013 = 17 * 4,118 + 7 leaves a partial
-# last group
-@pytest.mark.parametrize("S,mode,parts", [(140000, ppamd.SPLIT_AUTO, 2), (420000, ppamd.SPLIT_AUTO, 3),
-                                          (1048583, ppamd.SPLIT_AUTO, 3), (70001, ppamd.SPLIT_ON, 2),
-                                          (70013, ppamd.SPLIT_ON, 2)])
-def test_split_bit_identical(env, S, mode, parts):
+# last group; 1,572,865 scenes: two chunks of 3 parts (split_chunks); 3,001 scenes with K1 forced to
+# one lane per scene: the forced split's smallest batches (>= 2,048 scenes)
+@pytest.mark.parametrize("S,mode,parts,group", [(140000, ppamd.SPLIT_AUTO, 2, 0), (420000, ppamd.SPLIT_AUTO, 3, 0),
+                                                (1048583, ppamd.SPLIT_AUTO, 3, 0), (70001, ppamd.SPLIT_ON, 2, 0),
+                                                (70013, ppamd.SPLIT_ON, 2, 0), (1572865, ppamd.SPLIT_AUTO, 6, 0),
+                                                (3001, ppamd.SPLIT_ON, 2, 1)])
+def test_split_bit_identical(env, S, mode, parts, group):
     sc = ppamd.synth_host(env["m"], S, seed=S, first=S)
     idx = np.arange(7, S, 211)                    # speed-edge scenes: k_cand<true> groups in both halves
     sc["ego_speed_mph"][idx] = np.array([-0.0, 5e-324, 3e6, -3.0])[np.arange(len(idx)) % 4]
     prm = ppamd.default_params()
-    a = run(env, sc, prm, mode)
+    a = run(env, sc, prm, mode, group)
     assert ppamd.debug_get(ppamd.DBG_LAST_PARTS) == parts      # the split really ran
-    b = run(env, sc, prm, ppamd.SPLIT_OFF)
+    b = run(env, sc, prm, ppamd.SPLIT_OFF, group)
     assert ppamd.debug_get(ppamd.DBG_LAST_PARTS) == 1
     for k in a:
         x, y = np.asarray(a[k]), np.asarray(b[k])
         assert (x.view(np.uint8) == y.view(np.uint8)).all(), k
-    sub = np.unique(np.r_[0:300, S // 3 - 200:S // 3 + 200, S // 2 - 300:S // 2 + 300, 2 * S // 3 - 200:2 * S // 3 + 200,
-                          S - 300:S])
+    edges = [S * k // d for d in (2, 3, 6) for k in range(1, d)]     # part and chunk boundaries
+    sub = np.unique(np.concatenate([np.arange(0, min(300, S)), np.arange(max(S - 300, 0), S)] +
+                                   [np.arange(max(e - 150, 0), min(e + 150, S)) for e in edges]))
     part = {k: np.ascontiguousarray(v[..., sub]) for k, v in sc.items()}
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], part, prm, info=False)
     got = {k: (v[:, sub] if k in ("next_x", "next_y") else v[sub]) for k, v in a.items()}
     oracle_lib.compare(got, ref)
+
+
+def test_forced_split_small_batch_runs_one_stream(env):
+    """Below 2,048 scenes the forced split does not run (its parts could come out empty)."""
+    sc = ppamd.synth_host(env["m"], 1500, seed=9, first=9)
+    prm = ppamd.default_params()
+    a = run(env, sc, prm, ppamd.SPLIT_ON, 1)
+    assert ppamd.debug_get(ppamd.DBG_LAST_PARTS) == 1
+    b = run(env, sc, prm, ppamd.SPLIT_OFF, 1)
+    for k in a:
+        assert (np.asarray(a[k]).view(np.uint8) == np.asarray(b[k]).view(np.uint8)).all(), k

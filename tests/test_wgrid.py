@@ -65,7 +65,29 @@ def ego_points(wx, wy, rng):
     return np.concatenate(pts)
 
 
-def test_reference_waypoint_cells_vs_oracle(env):
+def run_gpu(env, sc, prm, group, waves=0):
+    """One evaluation with K1 forced to `group` lanes per scene (1: k_prep, the only K1 that reads
+    the cell table; 4: k_prep_g4, which always scans) and, for group 1, `waves` per SIMD."""
+    t = env["torch"]
+    S = sc["ego_x"].shape[0]
+    d = {k: t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
+    r = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"], info=True)
+    with ppamd.debug(ppamd.DBG_PREP_GROUP, group):
+        with ppamd.debug(ppamd.DBG_PREP_WAVES, waves):
+            ppamd.evaluate(env["m"], d, prm, r, device=0)
+    t.cuda.synchronize()
+    return ppamd.result_to_numpy(r)
+
+
+INFO_INT = ("ref_wp", "ego_lane")
+INFO_F64 = ("ego_s", "ego_d", "ref_ratio")
+
+
+@pytest.mark.parametrize("waves", [3, 4])
+def test_reference_waypoint_cells_vs_oracle(env, waves):
+    """The batch (~9,900 scenes) would take the grouped K1 (G = 8), which never reads the table
+    (ADVICE r5): K1 is forced to one lane per scene, in its 3-wave (table in LDS beside the map)
+    and 4-wave (global memory) builds, and pinned bit for bit against the grouped K1's full scan."""
     rng = np.random.default_rng(2025)
     p = ego_points(env["wx"], env["wy"], rng)
     S = p.shape[0]
@@ -74,17 +96,20 @@ def test_reference_waypoint_cells_vs_oracle(env):
     sc["ego_y"][:] = p[:, 1]
     sc["n_prev"][:] = 0                      # frame 0: the ego position is the telemetry's
     prm = ppamd.default_params(emit_paths=True)
-    t = env["torch"]
-    d = {k: t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
-    r = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"], info=True)
-    ppamd.evaluate(env["m"], d, prm, r, device=0)
-    t.cuda.synchronize()
-    got = ppamd.result_to_numpy(r)
+    got = run_gpu(env, sc, prm, 1, waves)
+    scan = run_gpu(env, sc, prm, 4)
     ref = oracle_lib.oracle_eval(env["olib"], env["wx"], env["wy"], sc, prm, info=True)
-    for k in ("ref_wp", "ego_lane"):
+    for k in INFO_INT:
         assert np.array_equal(got["info"][k], ref["info"][k]), k
-    for k in ("ego_s", "ego_d", "ref_ratio"):
-        a, b = got["info"][k], ref["info"][k]
+        assert np.array_equal(got["info"][k], scan["info"][k]), k
+    for k in INFO_F64:
+        a, b, c = got["info"][k], ref["info"][k], scan["info"][k]
         assert (a.view(np.uint64) == b.view(np.uint64)).all(), k
+        assert (a.view(np.uint64) == c.view(np.uint64)).all(), k
+    for k in ("winner", "n_out", "status", "path_len"):
+        assert np.array_equal(got[k], scan[k]), k
+    for k in ("paths", "next_x", "next_y", "cost"):
+        assert (got[k].view(np.uint64) == scan[k].view(np.uint64)).all(), k
     e = oracle_lib.compare(got, ref)
-    print(f"{S} egos: ref_wp / Frenet state bit-identical, max |dxy| {e:.3e} m")
+    print(f"{S} egos, K1 G=1 at {waves} waves: ref_wp / Frenet state bit-identical to the oracle and "
+          f"to the grouped K1's full scan, max |dxy| {e:.3e} m")

@@ -39,7 +39,7 @@ def main():
                                speed_offsets=[-6, -4, -3, -2, -1, 0, 2] if a.n_speeds == 8 else None)
     scenes = ppamd.synth_device(m, S, seed=0x5EED0001, device=0)
     res = ppamd.alloc_result(S, prm, xp="torch", device=torch.device("cuda", 0))
-    buf = (C.c_ulonglong * 64)()
+    buf = (C.c_ulonglong * 96)()
     lib.pp_diag_read(buf, 1)
     ppamd.evaluate(m, scenes, prm, res, device=0)
     torch.cuda.synchronize()

@@ -3,7 +3,13 @@ profiles/pmc_summary.json (read by bench.py for roofline.traffic).
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the bytes of wide
 coalesced streaming reads (x2 applied); WRITE_SIZE is exact for 16-B/lane streaming stores.
-Both counters are in KiB."""
+Both counters are in KiB.
+
+  python3 tools/pmc_summarize.py <dir> <tag> [parts]
+
+parts: the dispatches of each kernel per pp_eval call (a split batch launches every kernel once per
+part: 2 or 3 for a shard, 6 for BASELINE config 5's two chunks of 3 parts since round 6). The
+profiler reports counters per dispatch; a call's figures are the per-dispatch average x parts."""
 import csv
 import glob
 import json
@@ -15,6 +21,7 @@ from shape_tags import DOMINANT, lib_sha256, parse_tag
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 tag = sys.argv[2] if len(sys.argv) > 2 else None
+nparts = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
@@ -23,7 +30,7 @@ for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive
 summary = {}
 for k, d in vals.items():
     # rocprofv3 reports one row per dispatch per counter (already summed over XCDs/SEs)
-    summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
+    summary[k] = {c: sum(v) / len(v) * nparts for c, v in d.items()}
 print(json.dumps(summary, indent=1))
 
 
@@ -48,8 +55,8 @@ if tag:
             "hbm_bytes_per_launch": (2 * fetch + write) * 1024.0,
             "pipeline_bytes_per_step": sum(per_kernel.values()),
             "pipeline_bytes_by_kernel": per_kernel,
-            "fetch_kib_raw": fetch, "write_kib": write,
-            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), dominant-kernel instantiations summed",
+            "fetch_kib_raw": fetch, "write_kib": write, "parts": nparts,
+            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({src}, summarised into profiles/); FETCH_SIZE x2 (gfx950), dominant-kernel instantiations summed, per-dispatch averages x {nparts} dispatches per call",
             "counters": kc, "lib_sha256": lib_sha256()})
         json.dump(out, open(p, "w"), indent=1)
         print("wrote", p, tag)

@@ -24,10 +24,12 @@ DOMINANT = ("k_cand<", "k_cand_small", "k_step_small")
 
 
 def parse_tag(tag):
-    """Launch shape from a bench tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>]."""
-    m = re.match(r"k_cand_S(\d+)_C(\d+)_N(\d+)(_paths)?(?:_D(\d+))?$", tag)
+    """Launch shape from a bench tag k_cand_S<scenes>_C<cands>_N<points>[_paths][_D<draws>][_comfort]
+    (_comfort: the comfort cost mode, the data-dependent argmin; its kernels differ from the
+    reference decision's)."""
+    m = re.match(r"k_cand_S(\d+)_C(\d+)_N(\d+)(_paths)?(?:_D(\d+))?(_comfort)?$", tag)
     if not m:
-        raise SystemExit(f"tag {tag!r} is not k_cand_S<S>_C<C>_N<N>[_paths][_D<D>]")
+        raise SystemExit(f"tag {tag!r} is not k_cand_S<S>_C<C>_N<N>[_paths][_D<D>][_comfort]")
     S, C, N = int(m.group(1)), int(m.group(2)), int(m.group(3))
     return {"scenes": S, "candidates_per_scene": C, "n_points": N, "emit_paths": bool(m.group(4)),
-            "draws": int(m.group(5) or 1), "candidates_per_launch": S * C}
+            "draws": int(m.group(5) or 1), "comfort": bool(m.group(6)), "candidates_per_launch": S * C}
