@@ -3638,7 +3638,7 @@ bool step_fused_on() { return dbg(PP_DBG_SHAPE) != PP_SHAPE_CAND_SMALL; }
 // of the last call are read back with PP_DBG_LAST_PARTS.
 constexpr int64_t kSplitMin = 131072, kSplitMaxScenes = 1572864;
 #ifndef PP_SPLIT_BIG
-#define PP_SPLIT_BIG 1        // 0: batches beyond kSplitMaxScenes run on one stream (A/B builds)
+#define PP_SPLIT_BIG 0        // 1: batches beyond kSplitMaxScenes run as chunks (A/B builds)
 #endif
 constexpr int64_t kChunkScenes = 1048576;
 bool split_on(int64_t S) {
@@ -3655,12 +3655,14 @@ int split_parts(int64_t S) {
     if (PP_SPLIT_PARTS >= 2 && PP_SPLIT_PARTS <= kSplitMax) return PP_SPLIT_PARTS;
     return S > 393216 ? 3 : 2;
 }
-// chunks of a split batch: a batch beyond kSplitMaxScenes runs as ceil(S / 1,048,576) sequential
-// chunks of split_parts parts each (chunk c + 1 starts when every part of chunk c has ended).
-// Round 6, BASELINE config 5 (2,097,152 scenes), same box, alternating (tools/chunk_probe.py,
-// profiles/r06_chunk_probe.txt): one stream 9.89-9.99 ms, the 3-part split 9.90-9.93, two 1 M
-// chunks of 3 parts 9.78-9.81, four 512 k chunks 9.93-9.94; 6 parts pipelined over the 3 streams
-// without the join between chunks 10.00-10.04.
+// chunks of a split batch: a batch beyond kSplitMaxScenes, when split (PP_DBG_SPLIT 1, or
+// PP_SPLIT_BIG builds), runs as ceil(S / 1,048,576) sequential chunks of split_parts parts each
+// (chunk c + 1 starts when every part of chunk c has ended). Round 6 measured it for BASELINE
+// config 5 (2,097,152 scenes; tools/chunk_probe.py, profiles/r06_chunk_probe*.txt): two separate
+// pp_eval calls of 1,048,576 scenes (their own arrays) ran 9.78-9.87 ms against 9.79-9.99 for
+// one call on one stream, but the same chunks inside one call (the batch's own arrays) ran
+// 9.98-10.01 on the box where the separate calls took 9.85, and 6 parts pipelined over the 3
+// streams without the join 10.00-10.07: the full batch stays on one stream.
 int split_chunks(int64_t S) {
     if (S <= kSplitMaxScenes) return 1;
     const int64_t c = (S + kChunkScenes - 1) / kChunkScenes;

@@ -155,6 +155,13 @@ def test_shard_projection_arithmetic():
     assert pr["8"]["speedup"] == pytest.approx(0.010 / 0.00135)
     assert pr["8"]["efficiency"] == pytest.approx(0.010 / 0.00135 / 8)
     assert pr["4"]["shard_ms_per_step"] == pytest.approx(2.6)
+    # a shard faster than its share: the one-GPU baseline is the shards in sequence (like with like)
+    pr = bench.shard_projection(0.010, {2: 0.0048, 8: 0.0013})
+    assert pr["2"]["speedup"] == pytest.approx(2.0) and pr["2"]["efficiency"] <= 1.0
+    assert pr["2"]["one_gpu_policy"] == "2 shard calls in sequence"
+    assert pr["2"]["speedup_vs_one_call"] == pytest.approx(0.010 / 0.0048)
+    assert pr["8"]["speedup"] == pytest.approx(0.010 / 0.0013) and pr["8"]["one_gpu_policy"] == "one call"
+    assert all(v["efficiency"] <= 1.0 for v in pr.values())
 
 
 def test_ppamd_and_tools_hash_the_same_library():

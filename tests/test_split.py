@@ -1,6 +1,7 @@
 """The multi-stream split (pp_eval, include/pp.h PP_DBG_SPLIT): reference-mode batches of about a
 2-, 4- or 8-GPU shard's size run as 2 parts (up to 393,216 scenes) or 3 parts, each K1 -> K2 -> K4 on
-its own stream; larger batches (round 6) as sequential chunks of about 1,048,576 scenes, 3 parts each. The parts write disjoint ranges of every buffer and keep separate flagged-group
+its own stream; larger batches, when the split is forced, as sequential chunks of about 1,048,576
+scenes, 3 parts each (round 6). The parts write disjoint ranges of every buffer and keep separate flagged-group
 lists, so the results must be the one-stream launch's BIT FOR BIT, including the scenes routed to
 k_cand<true> and part boundaries that split no group; a sample is checked against the oracle."""
 import numpy as np
@@ -36,11 +37,11 @@ def run(env, sc, prm, mode, group=0):
 
 # (S, mode, parts): the automatic split (131,072 to 1,572,864 scenes) and the forced one below its
 # range (more than 65,536 scenes: one K1 lane per scene); 70,013 = 17 * 4,118 + 7 leaves a partial
-# last group; 1,572,865 scenes: two chunks of 3 parts (split_chunks); 3,001 scenes with K1 forced to
+# last group; 1,572,865 scenes, forced: two chunks of 3 parts (split_chunks); 3,001 scenes with K1 forced to
 # one lane per scene: the forced split's smallest batches (>= 2,048 scenes)
 @pytest.mark.parametrize("S,mode,parts,group", [(140000, ppamd.SPLIT_AUTO, 2, 0), (420000, ppamd.SPLIT_AUTO, 3, 0),
                                                 (1048583, ppamd.SPLIT_AUTO, 3, 0), (70001, ppamd.SPLIT_ON, 2, 0),
-                                                (70013, ppamd.SPLIT_ON, 2, 0), (1572865, ppamd.SPLIT_AUTO, 6, 0),
+                                                (70013, ppamd.SPLIT_ON, 2, 0), (1572865, ppamd.SPLIT_ON, 6, 0),
                                                 (3001, ppamd.SPLIT_ON, 2, 1)])
 def test_split_bit_identical(env, S, mode, parts, group):
     sc = ppamd.synth_host(env["m"], S, seed=S, first=S)

@@ -6,7 +6,7 @@ set -eo pipefail
 TAG=${1:-stalls}
 O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
-B="--steps 2 --warmup 1 --no-cpu-baseline --no-pcie --no-shard-projection"
+B="--steps 2 --warmup 1 --no-cpu-baseline --no-pcie --no-shard-projection --no-comfort"
 C="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU"
 for c in c5 c3 c4; do
   case $c in c5) X="";; c3) X="--emit-paths --n-speeds 8 --n-points 100 --scenes 262144";; c4) X="--draws 64 --n-speeds 1 --scenes 16384";; esac

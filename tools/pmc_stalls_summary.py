@@ -1,7 +1,7 @@
-"""Summarise tools/pmc_stalls.sh's passes into profiles/r05_pmc_stalls_final.json: per kernel the SQ
-counters per launch, VALU per wave and wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES, stamped with the
-SHA-256 of the library they measured (tools/shape_tags.lib_sha256).
-  python3 tools/pmc_stalls_summary.py TAG"""
+"""Summarise tools/pmc_stalls.sh's passes into a profiles/ file (default profiles/r06_pmc_stalls.json):
+per kernel the SQ counters per dispatch, VALU per wave and wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES,
+stamped with the SHA-256 of the library they measured (tools/shape_tags.lib_sha256).
+  python3 tools/pmc_stalls_summary.py TAG [OUT]"""
 import collections
 import csv
 import glob
@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from shape_tags import lib_sha256  # noqa: E402
 
 tag = sys.argv[1]
-out = {"what": "rocprofv3 --pmc SQ_* stall counters per kernel (per launch) of the final round-5 build; "
+dest = sys.argv[2] if len(sys.argv) > 2 else "profiles/r06_pmc_stalls.json"
+out = {"what": "rocprofv3 --pmc SQ_* stall counters per kernel (per dispatch) of the measured build; "
                "wait_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES, VALU/wave = SQ_INSTS_VALU / SQ_WAVES",
        "lib_sha256": lib_sha256(), "runs": {}}
 for c in ("c5", "c3", "c4"):
@@ -38,7 +39,7 @@ for c in ("c5", "c3", "c4"):
             e["wait_frac"] = e["SQ_WAIT_ANY"] / e["SQ_WAVE_CYCLES"]
         ks[k] = e
     out["runs"][c] = {"source": f"gpurun_out/{tag}/stall_{c}", "kernels": ks}
-json.dump(out, open("profiles/r05_pmc_stalls_final.json", "w"), indent=1)
+json.dump(out, open(dest, "w"), indent=1)
 for c, r in out["runs"].items():
     for k, e in r["kernels"].items():
         print(c, k, round(e.get("VALU_per_wave", 0)), round(e.get("wait_frac", 0), 3))
