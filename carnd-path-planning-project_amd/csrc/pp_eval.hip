@@ -2042,6 +2042,7 @@ __device__ __forceinline__ void emit_scene_pre(const pp_scene_batch& in, const p
 constexpr int kWinBlock = 64;
 constexpr int kWinKnots = 15;
 static_assert(PP_PREV_KEEP - 1 + 6 <= kWinKnots && kWinKnots <= kKP, "slot too small");
+constexpr int kWinRec = 5 * kWinKnots + 3;    // stored winner slot per scene (doubles): knots, 4 meta ints, pad (16-B records)
 template <bool kSlow, int kMode, int kEmitIn = 0, bool kPreA = false>
 __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch& in, const pp_params& P,
                                            const PrepV& pv, const pp_result& out, int SPB, int BPS,
@@ -2329,20 +2330,18 @@ __device__ __forceinline__ void cand_group(const MapG& mg, const pp_scene_batch&
             out.winner[s0 + tid] = best;
         }
         __syncthreads();
-        constexpr int kItems = 5 * kWinKnots + 4;      // x, y, a, b, c of each knot, then the meta
-        // item-major: a wave's lanes store consecutive scenes of one item (one row of the buffer)
+        // the scene's record: the LDS slot's knot-interleaved doubles (x, y, a, b, c of knot i at
+        // 5 i + field) as they lie, then the 4 meta ints; consecutive threads copy consecutive
+        // items of a scene, so a wave stores contiguous bytes
+        constexpr int kItems = 5 * kWinKnots + 4;
         for (int idx = tid; idx < nsc * kItems; idx += (int)blockDim.x) {
-            const int e = idx / nsc, w = idx - e * nsc;
+            const int w = idx / kItems, e = idx - w * kItems;
             if ((sSlow[w] != 0) != kSlow) continue;
             const int64_t s = s0 + w;
             const Slot sl = lds_slot(sX, nslot, sMeta, w * NL + sBest[w] / NS);
-            if (e < 5 * kWinKnots) {
-                const int f = e / kWinKnots, i = e - f * kWinKnots;
-                const double val = f == 0 ? sl.x(i) : f == 1 ? sl.y(i) : f == 2 ? sl.a(i) : f == 3 ? sl.b(i) : sl.c(i);
-                wslot[(int64_t)e * S + s] = val;
-            } else {
-                ((int*)(wslot + (int64_t)5 * kWinKnots * S))[(int64_t)(e - 5 * kWinKnots) * S + s] = sl.m(e - 5 * kWinKnots);
-            }
+            double* rec_s = wslot + s * kWinRec;
+            if (e < 5 * kWinKnots) rec_s[e] = sl.X[e];
+            else ((int*)(rec_s + 5 * kWinKnots))[e - 5 * kWinKnots] = sl.m(e - 5 * kWinKnots);
         }
     }
     if (kMode == 1 && emit_in) {
@@ -2467,10 +2466,11 @@ __global__ __launch_bounds__(kWinBlock) void k_winner(MapG mg, pp_scene_batch in
     winner_run<kSlow>(in, P, pv, out, s, v0, Sv, best, sl);
 }
 
-// Round 6: k_cand made the decision (out.winner) and stored the winner's spline slot
-// ([field * kWinKnots + knot][S] doubles, then the 4 meta ints [k][S]): no argmin, no spline build
-// and no LDS here, so the block is 256 lanes and occupancy is the registers' (k_winner holds 38 KB
-// of LDS per 64 lanes: one wave per SIMD).
+// Round 6: k_cand made the decision (out.winner) and stored the winner's spline slot (per scene
+// kWinRec doubles: the knot-interleaved x, y, a, b, c of k_cand's LDS slot, then the 4 meta ints):
+// no argmin, no spline build and no LDS here, so the block is 256 lanes and occupancy is the
+// registers' (k_winner holds 38 KB of LDS per 64 lanes: one wave per SIMD). A segment reload reads
+// one knot's 40 contiguous bytes, and the cache line holding them usually holds the next knot too.
 template <bool kSlow>
 __global__ __launch_bounds__(256) void k_winner_st(pp_scene_batch in, pp_params P, PrepV pv, pp_result out,
                                                    const double* wslot) {
@@ -2480,11 +2480,11 @@ __global__ __launch_bounds__(256) void k_winner_st(pp_scene_batch in, pp_params 
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t v0 = s * D;
     if (s >= S || ((pv.lim_mask[v0] & kLimSlow) != 0) != kSlow) return;
-    double* b = const_cast<double*>(wslot) + s;
-    const int64_t F = (int64_t)kWinKnots * S;
-    const Slot sl = {b, b + F, b + 2 * F, b + 3 * F, b + 4 * F, (int*)(const_cast<double*>(wslot) + 5 * F) + s, S, S};
+    double* b = const_cast<double*>(wslot) + s * kWinRec;
+    const Slot sl = {b, b + 1, b + 2, b + 3, b + 4, (int*)(b + 5 * kWinKnots), 5, 1};
     winner_run<kSlow>(in, P, pv, out, s, v0, Sv, out.winner[s], sl);
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // K4 (reference mode): next_x/next_y of the winner from its recorded local path — the output
@@ -3589,6 +3589,7 @@ int dev_init(pp_map* M, int device) {
 size_t prep_bytes(int64_t S) { return ((size_t)S * (kPrepD * 8 + kPrepI * 4) + 255) / 256 * 256; }
 // reference-mode winner record (k_cand -> k_emit): 3 x PP_MAX_POINTS x S doubles + 2 x S u64
 size_t rec_bytes(int64_t S) { return (size_t)S * (3 * PP_MAX_POINTS + 2) * 8 + 256; }
+static_assert(kWinRec <= 3 * PP_MAX_POINTS + 2, "the stored winner slots share the record's memory");
 double* rec_buf(void* rec) { return (double*)rec; }
 uint64_t* adj_buf(void* rec, int64_t cap) { return (uint64_t*)((double*)rec + 3 * PP_MAX_POINTS * cap); }
 
@@ -4111,7 +4112,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
         rec = rec_buf(W.rec);
         adjm = adj_buf(W.rec, W.rec_cap);
     }
-    // comfort mode and draws without paths, every scene's candidates in one block: k_cand makes the
+    // comfort mode without paths or draws, every scene's candidates in one block: k_cand makes the
     // decision and stores the winner's spline slot in the record's memory (616 B per scene of its
     // 3,088), k_winner_st re-runs the winner from it
     double* wslot = nullptr;
