@@ -343,6 +343,12 @@ constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
 #ifndef PP_CAND_WAVES2
 #define PP_CAND_WAVES2 PP_CAND_WAVES    // the all-paths instantiation k_cand<., 2>
 #endif
+#ifndef PP_UNROLL2
+#define PP_UNROLL2 1
+#endif
+#ifndef PP_PX_NULLTEST
+#define PP_PX_NULLTEST 0      // 1: mode 4 tests px per step as the other modes do (A/B)
+#endif
 #ifndef PP_ASIN_S
 #define PP_ASIN_S 0
 #endif
@@ -1705,229 +1711,251 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
 #endif
     // the divisions by 50 and by the ramp time: reciprocal + correction (k_cand<false>: unchecked)
 #define PP_DIV50(v) (kLarge ? ppm::div_rcp(v, 50.0, 0.02) : ppm::div50_nc(v))
-    while (arg < 50 && ng < room) {
-        PP_REGION("head");
-        PP_DIAGC(0, true);
-        PP_DIAGC(2, !(s_max(cur_t - sc.shift, 0.0) > sc.ttime));
-        double speed = sc_get_speed_r<kLarge>(sc, cur_t, rtt);
-        double dstep = PP_DIV50(speed);
-        const double x = arg + dstep;
-        // tk::spline::operator() (spline.h:375-396)
-        if (!(seg_lo < x && x <= seg_hi)) {
-            PP_REGION("seg");
-            // forward miss (x passed the cached segment's end; the first step starts from cnt = -1,
-            // seg_hi = -inf): x(cnt) = seg_hi < x is known, so the walk resumes one knot further
-            // and the bounds come from the walk's own reads — one LDS round trip for the knot and
-            // one for the coefficients, instead of the two loops' re-reads
-            if (__builtin_expect(x > seg_hi, 1)) {
-                double xlo = seg_hi, xhi;
-                cnt++;
-                for (;;) {
-                    xhi = cnt < nk ? sl.x(cnt) : __builtin_inf();
-                    if (!(xhi < x)) break;
-                    xlo = xhi;
+    // one step of the loop (src/main.cpp:911-1040): (uxp, uyp) the previous step's unit direction,
+    // prev_speed its speed; the step's own go to (uxn, uyn, psn). PP_UNROLL2 runs two steps per
+    // iteration with the two register sets alternating (no copies at the back edge)
+    auto step = [&](const double uxp, const double uyp, const double prev_speed, double& uxn, double& uyn,
+                    double& psn) __attribute__((always_inline)) {
+            PP_REGION("head");
+            PP_DIAGC(0, true);
+            PP_DIAGC(2, !(s_max(cur_t - sc.shift, 0.0) > sc.ttime));
+            double speed = sc_get_speed_r<kLarge>(sc, cur_t, rtt);
+            double dstep = PP_DIV50(speed);
+            const double x = arg + dstep;
+            // tk::spline::operator() (spline.h:375-396)
+            if (!(seg_lo < x && x <= seg_hi)) {
+                PP_REGION("seg");
+                // forward miss (x passed the cached segment's end; the first step starts from cnt = -1,
+                // seg_hi = -inf): x(cnt) = seg_hi < x is known, so the walk resumes one knot further
+                // and the bounds come from the walk's own reads — one LDS round trip for the knot and
+                // one for the coefficients, instead of the two loops' re-reads
+                if (__builtin_expect(x > seg_hi, 1)) {
+                    double xlo = seg_hi, xhi;
                     cnt++;
-                }
-                seg_lo = xlo;
-                seg_hi = xhi;
-                const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
-                sx = cnt > 0 ? xlo : xhi;
-                sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
-            } else {
-                PP_REGION("segback");
-                PP_DIAGC(21, true);
-                if (cnt < 0) cnt = 0;
-                while (cnt < nk && sl.x(cnt) < x) cnt++;
-                while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
-                const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
-                seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
-                seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
-                sx = sl.x(idx); sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
-            }
-            PP_DIAGC(1, true);
-        }
-        PP_REGION("eval");
-        const double h = x - sx;
-        // the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0 (0 h + b = b, and
-        // at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the last knot, whose a is
-        // 0 (spline.h:367): one polynomial form for every step
-        const double y = ((sa_ * h + sb) * h + sc_) * h + sy;
-        double d, rd;
-        const bool dok = ppm::sqrt_rd((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y), d, rd);
-        double acc = fabs(speed - prev_speed) * 50;
-        // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
-        // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
-        double ux, uy;
-        {
-            PP_REGION("dir");
-            const double ddx = x - pos_x, ddy = y - pos_y;
-            ux = ddx * rd; uy = ddy * rd;
-            PP_DIAGC(18, !dok);
-            if (__builtin_expect(!dok, 0)) {        // d == 0 implies !dok (q = 0 < 2^-900)
-                PP_REGION("dirfix");
-                if (d == 0) { ux = 1.0; uy = 0.0; }
-                // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only
-                // in k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
-                // atan2(dy, dx) still has one; normalise the step scaled by its larger component
-                if (d == __builtin_inf() && fabs(ddx) <= 0x1.fffffffffffffp1023 &&
-                    fabs(ddy) <= 0x1.fffffffffffffp1023) {
-                    const double m = s_max(fabs(ddx), fabs(ddy));
-                    const double a = ddx / m, b = ddy / m;
-                    const double n = sqrt(a * a + b * b);
-                    ux = a / n; uy = b / n;
-                }
-            }
-        }
-        PP_REGION("cross");
-        const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
-        // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
-        // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
-        double adiff;
-        PP_DIAGC(3, !((PP_NARROW(dt, cr)) || speed == 0));
-        PP_DIAGC(8, ng == 0 && !(PP_NARROW(dt, cr)));
-        PP_DIAGC(9, !(dt > 0));
-        if (__builtin_expect(PP_NARROW(dt, cr), 1)) {
-            PP_REGION("asin");
-            adiff = (((PP_ASIN_S == 2 ? ppm::asin_small_b(cr) : PP_ASIN_S ? ppm::asin_small_s(cr) : ppm::asin_small(cr)) + 3 * kPi) - 2 * kPi) - kPi;
-        } else {
-            PP_REGION("wide");
-            // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
-            adiff = ppm::fmod_2pi_small(ppm::atan2_unit(cr, dt) + 3 * kPi) - kPi;
-        }
-        PP_REGION("acc");
-        const double cacc = speed * 50 * fabs(adiff);
-        double eff_c = cacc;
-#ifdef PP_LIMCENSUS
-        bool cen_r1, cen_r2;
-        {
-            const double spd_r = sc_get_speed(sc, cur_t);                 // :919 (IEEE division)
-            const double ast_r = ppg::atan2(y - pos_y, x - pos_x);        // :933
-            const double adf_r = ppm::fmod_2pi(ast_r - ref_pa + 3 * kPi) - kPi;   // :934
-            const double acc_r = fabs(spd_r - prev_speed) * 50, cacc_r = spd_r * 50 * fabs(adf_r);
-            const double mx = P.maximum_acc, tol = 1e-12 * fabs(mx);
-            cen_r1 = acc_r + cacc_r > mx;                                 // :941
-            cen_r2 = cen_r1;
-            if (cen_r1 && spd_r > prev_speed) {                           // :945-971, then :972
-                double na_r = mx - cacc_r;
-                if (na_r < 0) na_r = 0;
-                cen_r2 = na_r + cacc_r > mx;
-            }
-            PP_CEN(26, fabs(acc + cacc - mx) <= tol);
-            PP_CEN(27, fabs(acc_r + cacc_r - mx) <= tol);
-            PP_CEN(28, (acc + cacc > mx) != cen_r1);
-            PP_CEN(32, __double_as_longlong(cacc) != __double_as_longlong(cacc_r));
-            PP_CEN(33, __double_as_longlong(speed) != __double_as_longlong(spd_r));
-            ref_pa = ast_r;
-        }
-#endif
-        PP_DIAGC(4, acc + cacc > P.maximum_acc);
-        PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
-        PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
-        PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
-        if (acc + cacc > P.maximum_acc) {
-            PP_REGION("lim");
-            if (speed > prev_speed) {                                   // :945-971
-                PP_REGION("ovr");
-                // (inside this block acc + cacc > max held: neither is NaN; k_cand<false>'s
-                // operands are finite, so the clamp is v_max_f64)
-                double na = P.maximum_acc - cacc;
-                if (kLarge) { if (na < 0) na = 0; } else na = __builtin_fmax(na, 0.0);
-                const double ns = prev_speed + PP_DIV50(na);
-                sc_override_r<kLarge>(sc, cur_t, ns, rds);
-                speed = ns;
-                sc.ttime += 0.02;
-                rtt = PP_RCP1 ? ppm::rcp_nr1(sc.ttime) : ppm::rcp_nr(sc.ttime);
-                dstep = PP_DIV50(speed);
-                acc = na;
-                R.flags |= PP_ST_ACC_OVERRIDE;
-            }
-            PP_DIAGC(6, acc + cacc > P.maximum_acc);
-            PP_CEN(29, true);
-            PP_CEN(30, fabs(acc + cacc - P.maximum_acc) <= 1e-12 * fabs(P.maximum_acc));
-            PP_CEN(31, cen_r1 && (acc + cacc > P.maximum_acc) != cen_r2);
-            PP_REGION("lim2");
-            if (acc + cacc > P.maximum_acc) {                           // :972-1018
-                PP_REGION("adj");
-                double nc = P.maximum_acc - acc;
-                if (kLarge) { if (nc < 0) nc = 0; } else nc = __builtin_fmax(nc, 0.0);
-                if (kOutMode == 2) {
-                    // the output frame turns about the current point (src/main.cpp:986-997)
-                    double cr, sr;
-                    turn_sincos<kLarge>(turn_angle<kLarge>(nc, speed, adiff), sr, cr);
-                    frame_turn(F, pos_x, pos_y, cr, sr);
-                } else if (kOutMode == 4) {
-#if PP_PATHS_INC
-                    PP_DIAGC(19, !(!kLarge && PP_NARROW(dt, cr)));
-                    PP_DIAGC(23, !kLarge && PP_NARROW(dt, cr));
-                    if (!kLarge && PP_NARROW(dt, cr)) {
-                        PP_REGION("adjn");
-                        turn_narrow(F.ca, F.sa, nc, speed, adiff, dt, cr);
-                    } else {
-                        PP_REGION("adjwide");
-                        double crr, srr;
-                        turn_sincos<kLarge>(kLarge ? turn_angle<true>(nc, speed, adiff)
-                                                   : turn_angle_fast(nc, speed, adiff), srr, crr);
-                        frame_rot(F.ca, F.sa, crr, srr);
+                    for (;;) {
+                        xhi = cnt < nk ? sl.x(cnt) : __builtin_inf();
+                        if (!(xhi < x)) break;
+                        xlo = xhi;
+                        cnt++;
                     }
-#else
-                    double cr, sr;
-                    turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), sr, cr);
-                    frame_turn_at(F, pos_x, pos_y, opx, opy, cr, sr);
-#endif
+                    seg_lo = xlo;
+                    seg_hi = xhi;
+                    const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+                    sx = cnt > 0 ? xlo : xhi;
+                    sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
+                } else {
+                    PP_REGION("segback");
+                    PP_DIAGC(21, true);
+                    if (cnt < 0) cnt = 0;
+                    while (cnt < nk && sl.x(cnt) < x) cnt++;
+                    while (cnt > 0 && !(sl.x(cnt - 1) < x)) cnt--;
+                    const int idx = cnt - 1 > 0 ? cnt - 1 : 0;
+                    seg_lo = cnt > 0 ? sl.x(cnt - 1) : -__builtin_inf();
+                    seg_hi = cnt < nk ? sl.x(cnt) : __builtin_inf();
+                    sx = sl.x(idx); sa_ = cnt == 0 ? 0.0 : sl.a(idx); sb = sl.b(idx); sc_ = sl.c(idx); sy = sl.y(idx);
                 }
-                if (kOutMode == 3 && kRec) {
-                    // the turn angle for k_emit's replay of the output frame
-                    double* rp = rec_rot(rec - rs, rstride, ng, ws, rs);
-                    if (PP_CHKP(rp, rec, nrec, 6))
-                        PP_ST(rp, turn_angle<kLarge>(nc, speed, adiff));   // rot (src/main.cpp:986)
-                    const uint64_t bit = 1ull << (ng & 63);
-                    if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
-                }
-                eff_c = nc;
-                R.flags |= PP_ST_CURV_ADJUST;
+                PP_DIAGC(1, true);
             }
-        }
-        PP_REGION("tail");
-        cur_t += 0.02;
-        prev_speed = speed;
-        uxp = ux; uyp = uy;
-        double sp_step, dpy;
-        if (kLarge) {
-            sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
-            dpy = ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok);
-        } else {          // ppm::div_rcp_d for both numerators, one !dok branch
-            const double nx = (x - pos_x) * dstep, ny = (y - pos_y) * dstep;
-            const double qx = nx * rd, qy = ny * rd;
-            sp_step = __builtin_fma(__builtin_fma(-qx, d, nx), rd, qx);
-            dpy = __builtin_fma(__builtin_fma(-qy, d, ny), rd, qy);
-            if (__builtin_expect(!dok, 0)) { PP_REGION("tailfix"); sp_step = nx / d; dpy = ny / d; }
-        }
-        PP_REGION("tail2");
-        pos_y += dpy;
-        arg += sp_step;
-        pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
-        if (kOutMode != 0 && kOut) {
-            PP_REGION("out");
-            PP_DIAGC(22, wx != nullptr);
-            double ox, oy;
-#if PP_PATHS_INC
-            if (kOutMode == 4) { ox = opx; oy = opy; frame_step(F.ca, F.sa, sp_step, dpy, ox, oy); }
-#else
-            if (kOutMode == 4) frame_pt_fma(F, pos_x, pos_y, ox, oy);
+            PP_REGION("eval");
+            const double h = x - sx;
+            // the left extrapolation (cnt == 0: x <= x0) is the cubic form with a = 0 (0 h + b = b, and
+            // at x == x0, h = 0 both give y0); the right one (cnt == nk) uses the last knot, whose a is
+            // 0 (spline.h:367): one polynomial form for every step
+            const double y = ((sa_ * h + sb) * h + sc_) * h + sy;
+            double d, rd;
+            const bool dok = ppm::sqrt_rd((x - pos_x) * (x - pos_x) + (y - pos_y) * (y - pos_y), d, rd);
+            double acc = fabs(speed - prev_speed) * 50;
+            // the turn from the previous step direction u_prev to u = (dx, dy) / d (ppm::asin_small;
+            // wide turns: atan2(u_prev x u, u_prev . u)). d == 0: atan2(+0, +0) = 0, u = (1, 0).
+            double ux, uy;
+            {
+                PP_REGION("dir");
+                const double ddx = x - pos_x, ddy = y - pos_y;
+                ux = ddx * rd; uy = ddy * rd;
+                PP_DIAGC(18, !dok);
+                if (__builtin_expect(!dok, 0)) {        // d == 0 implies !dok (q = 0 < 2^-900)
+                    PP_REGION("dirfix");
+                    if (d == 0) { ux = 1.0; uy = 0.0; }
+                    // finite step whose squared length overflows (speeds of ~1e150 m/s and more, only
+                    // in k_cand<true> scenes): rd = 0 would leave no direction, where the reference's
+                    // atan2(dy, dx) still has one; normalise the step scaled by its larger component
+                    if (d == __builtin_inf() && fabs(ddx) <= 0x1.fffffffffffffp1023 &&
+                        fabs(ddy) <= 0x1.fffffffffffffp1023) {
+                        const double m = s_max(fabs(ddx), fabs(ddy));
+                        const double a = ddx / m, b = ddy / m;
+                        const double n = sqrt(a * a + b * b);
+                        ux = a / n; uy = b / n;
+                    }
+                }
+            }
+            PP_REGION("cross");
+            const double cr = uxp * uy - uyp * ux, dt = uxp * ux + uyp * uy;
+            // the reference's wrap fmod(a + 3 pi, 2 pi) - pi: for |a| <= kStepSinMax, a + 3 pi lies in
+            // [2 pi, 4 pi), where fmod is the exact subtraction of 2 pi (ppm::fmod_2pi's second case)
+            double adiff;
+            PP_DIAGC(3, !((PP_NARROW(dt, cr)) || speed == 0));
+            PP_DIAGC(8, ng == 0 && !(PP_NARROW(dt, cr)));
+            PP_DIAGC(9, !(dt > 0));
+            if (__builtin_expect(PP_NARROW(dt, cr), 1)) {
+                PP_REGION("asin");
+                adiff = (((PP_ASIN_S == 2 ? ppm::asin_small_b(cr) : PP_ASIN_S ? ppm::asin_small_s(cr) : ppm::asin_small(cr)) + 3 * kPi) - 2 * kPi) - kPi;
+            } else {
+                PP_REGION("wide");
+                // cr, dt: components of unit vectors (finite, never both zero; NaN propagates)
+                adiff = ppm::fmod_2pi_small(ppm::atan2_unit(cr, dt) + 3 * kPi) - kPi;
+            }
+            PP_REGION("acc");
+            const double cacc = speed * 50 * fabs(adiff);
+            double eff_c = cacc;
+    #ifdef PP_LIMCENSUS
+            bool cen_r1, cen_r2;
+            {
+                const double spd_r = sc_get_speed(sc, cur_t);                 // :919 (IEEE division)
+                const double ast_r = ppg::atan2(y - pos_y, x - pos_x);        // :933
+                const double adf_r = ppm::fmod_2pi(ast_r - ref_pa + 3 * kPi) - kPi;   // :934
+                const double acc_r = fabs(spd_r - prev_speed) * 50, cacc_r = spd_r * 50 * fabs(adf_r);
+                const double mx = P.maximum_acc, tol = 1e-12 * fabs(mx);
+                cen_r1 = acc_r + cacc_r > mx;                                 // :941
+                cen_r2 = cen_r1;
+                if (cen_r1 && spd_r > prev_speed) {                           // :945-971, then :972
+                    double na_r = mx - cacc_r;
+                    if (na_r < 0) na_r = 0;
+                    cen_r2 = na_r + cacc_r > mx;
+                }
+                PP_CEN(26, fabs(acc + cacc - mx) <= tol);
+                PP_CEN(27, fabs(acc_r + cacc_r - mx) <= tol);
+                PP_CEN(28, (acc + cacc > mx) != cen_r1);
+                PP_CEN(32, __double_as_longlong(cacc) != __double_as_longlong(cacc_r));
+                PP_CEN(33, __double_as_longlong(speed) != __double_as_longlong(spd_r));
+                ref_pa = ast_r;
+            }
+    #endif
+            PP_DIAGC(4, acc + cacc > P.maximum_acc);
+            PP_DIAGC(10 + (ng == 0 ? 0 : ng == 1 ? 1 : ng < 5 ? 2 : ng < 10 ? 3 : ng < 20 ? 4 : 5), acc + cacc > P.maximum_acc);
+            PP_DIAGC(5, acc + cacc > P.maximum_acc && speed > prev_speed);
+            PP_DIAGC(7, acc + cacc > P.maximum_acc && speed > prev_speed && dcls == 1);
+            if (acc + cacc > P.maximum_acc) {
+                PP_REGION("lim");
+                if (speed > prev_speed) {                                   // :945-971
+                    PP_REGION("ovr");
+                    // (inside this block acc + cacc > max held: neither is NaN; k_cand<false>'s
+                    // operands are finite, so the clamp is v_max_f64)
+                    double na = P.maximum_acc - cacc;
+                    if (kLarge) { if (na < 0) na = 0; } else na = __builtin_fmax(na, 0.0);
+                    const double ns = prev_speed + PP_DIV50(na);
+                    sc_override_r<kLarge>(sc, cur_t, ns, rds);
+                    speed = ns;
+                    sc.ttime += 0.02;
+                    rtt = PP_RCP1 ? ppm::rcp_nr1(sc.ttime) : ppm::rcp_nr(sc.ttime);
+                    dstep = PP_DIV50(speed);
+                    acc = na;
+                    R.flags |= PP_ST_ACC_OVERRIDE;
+                }
+                PP_DIAGC(6, acc + cacc > P.maximum_acc);
+                PP_CEN(29, true);
+                PP_CEN(30, fabs(acc + cacc - P.maximum_acc) <= 1e-12 * fabs(P.maximum_acc));
+                PP_CEN(31, cen_r1 && (acc + cacc > P.maximum_acc) != cen_r2);
+                PP_REGION("lim2");
+                if (acc + cacc > P.maximum_acc) {                           // :972-1018
+                    PP_REGION("adj");
+                    double nc = P.maximum_acc - acc;
+                    if (kLarge) { if (nc < 0) nc = 0; } else nc = __builtin_fmax(nc, 0.0);
+                    if (kOutMode == 2) {
+                        // the output frame turns about the current point (src/main.cpp:986-997)
+                        double cr, sr;
+                        turn_sincos<kLarge>(turn_angle<kLarge>(nc, speed, adiff), sr, cr);
+                        frame_turn(F, pos_x, pos_y, cr, sr);
+                    } else if (kOutMode == 4) {
+    #if PP_PATHS_INC
+                        PP_DIAGC(19, !(!kLarge && PP_NARROW(dt, cr)));
+                        PP_DIAGC(23, !kLarge && PP_NARROW(dt, cr));
+                        if (!kLarge && PP_NARROW(dt, cr)) {
+                            PP_REGION("adjn");
+                            turn_narrow(F.ca, F.sa, nc, speed, adiff, dt, cr);
+                        } else {
+                            PP_REGION("adjwide");
+                            double crr, srr;
+                            turn_sincos<kLarge>(kLarge ? turn_angle<true>(nc, speed, adiff)
+                                                       : turn_angle_fast(nc, speed, adiff), srr, crr);
+                            frame_rot(F.ca, F.sa, crr, srr);
+                        }
+    #else
+                        double cr, sr;
+                        turn_sincos<kLarge>(turn_angle_fast(nc, speed, adiff), sr, cr);
+                        frame_turn_at(F, pos_x, pos_y, opx, opy, cr, sr);
+    #endif
+                    }
+                    if (kOutMode == 3 && kRec) {
+                        // the turn angle for k_emit's replay of the output frame
+                        double* rp = rec_rot(rec - rs, rstride, ng, ws, rs);
+                        if (PP_CHKP(rp, rec, nrec, 6))
+                            PP_ST(rp, turn_angle<kLarge>(nc, speed, adiff));   // rot (src/main.cpp:986)
+                        const uint64_t bit = 1ull << (ng & 63);
+                        if (ng < 64) R.adj0 |= bit; else R.adj1 |= bit;
+                    }
+                    eff_c = nc;
+                    R.flags |= PP_ST_CURV_ADJUST;
+                }
+            }
+            PP_REGION("tail");
+            cur_t += 0.02;
+            psn = speed;
+            uxn = ux; uyn = uy;
+            double sp_step, dpy;
+            if (kLarge) {
+                sp_step = ppm::div_rcp_n((x - pos_x) * dstep, d, rd, dok);
+                dpy = ppm::div_rcp_n((y - pos_y) * dstep, d, rd, dok);
+            } else {          // ppm::div_rcp_d for both numerators, one !dok branch
+                const double nx = (x - pos_x) * dstep, ny = (y - pos_y) * dstep;
+                const double qx = nx * rd, qy = ny * rd;
+                sp_step = __builtin_fma(__builtin_fma(-qx, d, nx), rd, qx);
+                dpy = __builtin_fma(__builtin_fma(-qy, d, ny), rd, qy);
+                if (__builtin_expect(!dok, 0)) { PP_REGION("tailfix"); sp_step = nx / d; dpy = ny / d; }
+            }
+            PP_REGION("tail2");
+            pos_y += dpy;
+            arg += sp_step;
+            pos_x = arg;      // == pos_x + sp_step: both start at 0 and add the same sp_step (:1027-1031)
+            if (kOutMode != 0 && kOut) {
+                PP_REGION("out");
+                PP_DIAGC(22, wx != nullptr);
+                double ox, oy;
+    #if PP_PATHS_INC
+                if (kOutMode == 4) { ox = opx; oy = opy; frame_step(F.ca, F.sa, sp_step, dpy, ox, oy); }
+    #else
+                if (kOutMode == 4) frame_pt_fma(F, pos_x, pos_y, ox, oy);
+    #endif
+                else frame_pt(F, pos_x, pos_y, ox, oy);
+                if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { PP_REGION("outw"); wx[ng * ws] = ox; wy[ng * ws] = oy; }
+                PP_REGION("out2");
+                // (mode 4 is k_cand's all-paths output: px is never null there, and a per-lane null
+                // test would cost two VALU per step)
+                if (((kOutMode == 4 && !PP_PX_NULLTEST) || px) && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
+                    st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
+                if (kOutMode == 4) { opx = ox; opy = oy; }
+            }
+            if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
+            PP_REGION("latch");
+            ng++;
+            R.acc_sum += acc + eff_c;
+            R.travelled += dstep;
+        };
+#if PP_UNROLL2
+    double uxq = 0, uyq = 0, psq = 0;
+    while (arg < 50 && ng < room) {
+        step(uxp, uyp, prev_speed, uxq, uyq, psq);
+        if (!(arg < 50 && ng < room)) break;
+        step(uxq, uyq, psq, uxp, uyp, prev_speed);
+#if PP_UNROLL2 > 1
+        if (!(arg < 50 && ng < room)) break;
+        step(uxp, uyp, prev_speed, uxq, uyq, psq);
+        if (!(arg < 50 && ng < room)) break;
+        step(uxq, uyq, psq, uxp, uyp, prev_speed);
 #endif
-            else frame_pt(F, pos_x, pos_y, ox, oy);
-            if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { PP_REGION("outw"); wx[ng * ws] = ox; wy[ng * ws] = oy; }
-            PP_REGION("out2");
-            if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
-                st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
-            if (kOutMode == 4) { opx = ox; opy = oy; }
-        }
-        if (kOutMode == 3 && kRec && PP_CHKP(rec_px(rec - rs, rstride, ng, ws, rs), rec, nrec, 4) && PP_CHKP(rec_py(rec - rs, rstride, ng, ws, rs), rec, nrec, 5)) rec_st(rec - rs, rstride, ng, ws, rs, pos_x, pos_y);
-        PP_REGION("latch");
-        ng++;
-        R.acc_sum += acc + eff_c;
-        R.travelled += dstep;
     }
+#else
+    while (arg < 50 && ng < room) step(uxp, uyp, prev_speed, uxp, uyp, prev_speed);
+#endif
     PP_REGION("end");
     R.ng = ng;
     return R;
