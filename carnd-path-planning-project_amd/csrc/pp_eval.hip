@@ -346,9 +346,6 @@ constexpr int kPrepWaves = 3;      // k_prep waves per SIMD (kW4: 4)
 #ifndef PP_UNROLL2
 #define PP_UNROLL2 1
 #endif
-#ifndef PP_PX_NULLTEST
-#define PP_PX_NULLTEST 0      // 1: mode 4 tests px per step as the other modes do (A/B)
-#endif
 #ifndef PP_ASIN_S
 #define PP_ASIN_S 0
 #endif
@@ -1928,9 +1925,7 @@ __device__ CandRes run_candidate(const pp_params& P, const Slot& sl, double cx, 
                 else frame_pt(F, pos_x, pos_y, ox, oy);
                 if (wx && PP_CHKP(wx + ng * ws, nx, nnext, 1) && PP_CHKP(wy + ng * ws, ny, nnext, 2)) { PP_REGION("outw"); wx[ng * ws] = ox; wy[ng * ws] = oy; }
                 PP_REGION("out2");
-                // (mode 4 is k_cand's all-paths output: px is never null there, and a per-lane null
-                // test would cost two VALU per step)
-                if (((kOutMode == 4 && !PP_PX_NULLTEST) || px) && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
+                if (px && PP_CHKP(px + ng * ps, paths, npaths, 3) && PP_CHKP(px + ng * ps + 1, paths, npaths, 3))
                     st_xy(px + ng * ps, ox, oy);      // one 16-B store (x, y)
                 if (kOutMode == 4) { opx = ox; opy = oy; }
             }
