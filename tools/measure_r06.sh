@@ -19,6 +19,7 @@ NP="--no-cpu-baseline --no-pcie --no-shard-projection --no-comfort"
 if [ "$PART" = A ]; then
   bash tools/gpu_suite.sh $TAG/suite
   rp() { name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/$name -o run -- python3 $ROOT/bench.py $NP "$@" > $OUT/$name.json 2> $OUT/$name.err; echo "rocprof $name done"; }
+  echo '{}' > profiles/rocprof_summary.json       # only this build's kernel traces
   rp stats5
   rp stats5_comfort --comfort
   rp stats3 --emit-paths --n-speeds 8 --n-points 100 --scenes 262144
@@ -42,6 +43,7 @@ if [ "$PART" = A ]; then
   exit 0
 fi
 # part B
+echo '{}' > profiles/pmc_summary.json             # only this build's counters
 pm() { name=$1; tag=$2; parts=$3; shift 3; bash tools/pmc.sh $OUT/$name --steps 2 --warmup 1 $NP "$@" > $OUT/$name.log 2>&1; python3 tools/pmc_summarize.py $OUT/$name $tag $parts > $OUT/${name}_summary.txt; echo "pmc $name done"; }
 pm pmc5 k_cand_S2097152_C15_N50 1
 pm pmc5_comfort k_cand_S2097152_C15_N50_comfort 1 --comfort

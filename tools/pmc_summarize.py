@@ -35,7 +35,7 @@ print(json.dumps(summary, indent=1))
 
 
 STEP_KERNELS = ("k_prep", "k_prep_g2", "k_prep_g4", "k_prep_g8", "k_prep_g16", "k_cand", "k_cand_small",
-                "k_step_small", "k_emit", "k_winner")
+                "k_step_small", "k_emit", "k_winner", "k_winner_st")
 if tag:
     shape = parse_tag(tag)
     parts = [v for k, v in summary.items() if k.startswith(DOMINANT)]
