@@ -240,7 +240,7 @@ def parse(argv=None):
                     help="chunks of the host-buffer pipeline (H2D / evaluate / D2H overlapped across chunks)")
     ap.add_argument("--debug", action="append", default=[], metavar="KEY=VALUE",
                     help="library debug switch for A/B runs (include/pp.h PP_DBG_*): prep_group=G, "
-                         "prep_waves=3|4, shape=1|2|3, split=1|2; recorded in config.debug, which marks the line not reportable")
+                         "prep_waves=3|4, shape=1|2|3, split=1|2, sort_cars=1|2; recorded in config.debug, which marks the line not reportable")
     ap.add_argument("--no-comfort", action="store_true",
                     help="skip the comfort-mode (data-dependent argmin) side measurement of config 5 (1 GPU)")
     ap.add_argument("--no-shard-projection", action="store_true",
@@ -514,7 +514,7 @@ def main(argv=None):
     import torch
     import ppamd
     keys = {"prep_group": ppamd.DBG_PREP_GROUP, "prep_waves": ppamd.DBG_PREP_WAVES, "shape": ppamd.DBG_SHAPE,
-            "split": ppamd.DBG_SPLIT}
+            "split": ppamd.DBG_SPLIT, "sort_cars": ppamd.DBG_SORT_CARS}
     for kv in a.debug:
         k, _, v = kv.partition("=")
         ppamd.debug_set(keys[k], int(v))

@@ -911,10 +911,94 @@ __device__ __forceinline__ void car_noise(const pp_params& P, int64_t s, int dra
 #ifndef PP_SORT_DMAX
 #define PP_SORT_DMAX 16          // k_prep sorts a scene's rows nearest first below this many draws
 #endif
-template <bool kLdsMap, bool kW4 = false>
+#ifndef PP_SORT_K0
+#define PP_SORT_K0 0             // 1: k_sort_cars by default (PP_DBG_SORT_CARS switches it per call)
+#endif
+// K0 (round 6, PP_SORT_K0): each scene's cars in k_prep's visiting order, visit-major.
+// k_prep visits a scene's rows nearest first (below), and read them in that order straight from the
+// batch's row-major arrays: a wave's load of visit k gathers 64 scenes' rows from up to 12 rows,
+// each cache line partly used and fetched again at later visits (FETCH ~7x the scene record,
+// DESIGN.md §4). k_sort_cars computes the same order (the same keys, the same network, the same
+// identity-order rules) and writes the rows permuted into visit-major arrays x[k][s], ... through a
+// per-lane LDS column, so k_prep's visit k reads 64 consecutive values per field. Only for batches
+// without a car table, fewer than PP_SORT_DMAX draws and at most 16 rows per scene (the host's
+// condition); the values are copies, so k_prep's results are the same bits.
+struct SortedCars {
+    double *x, *y, *vx, *vy;      // [k][S], k < rows: the k-th visited row's fields
+    int* id;                      // [k][S]
+    uint64_t* order;              // [S]: the visiting order, one row index per nibble
+    int rows;                     // min(car_stride, 16); 0: not in use
+};
+__device__ __forceinline__ uint64_t car_order(const pp_scene_batch& in, int64_t S, int64_t s, double ex,
+                                              double ey, int iters) {
+    uint64_t order = 0xFEDCBA9876543210ull;
+    if (!(iters > 1 && iters <= 16)) return order;
+    uint32_t key[16];
+    bool neg = false;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        key[j] = 0xFFFFFFF0u | (uint32_t)j;
+        if (j < iters) {
+            const int64_t ix = (int64_t)j * S + s;
+            const double dx = in.car_x[ix] - ex, dy = in.car_y[ix] - ey;
+            const float f = (float)(dx * dx + dy * dy);
+            key[j] = (__float_as_uint(f) & ~15u) | (uint32_t)j;
+            neg |= in.car_id[ix] < 0;
+        }
+    }
+#pragma unroll
+    for (int pw = 1; pw < 16; pw <<= 1)
+#pragma unroll
+        for (int k = pw; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % pw; j < 16 - k; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; i++)
+                    if ((i + j) / (2 * pw) == (i + j + k) / (2 * pw)) {
+                        const uint32_t lo = key[i + j] < key[i + j + k] ? key[i + j] : key[i + j + k];
+                        const uint32_t hi = key[i + j] < key[i + j + k] ? key[i + j + k] : key[i + j];
+                        key[i + j] = lo; key[i + j + k] = hi;
+                    }
+    if (neg) return order;
+    order = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) order |= (uint64_t)(key[j] & 15u) << (4 * j);
+    return order;
+}
+__global__ __launch_bounds__(256) void k_sort_cars(pp_scene_batch in, SortedCars sc, int64_t s0, int64_t s1) {
+    __shared__ double col[16 * 256];          // this lane's rows of one field: col[j * 256 + lane]
+    const int64_t S = in.n_scenes;
+    const int t = threadIdx.x;
+    const int64_t s = s0 + (int64_t)blockIdx.x * 256 + t;
+    if (s >= s1) return;                      // (no barrier below: every lane uses its own column)
+    int iters = in.n_cars[s];
+    if (iters > in.car_stride) iters = in.car_stride;
+    // the ego position k_prep's keys use (prep_ego: the last kept point when 10 are kept)
+    const int np = in.n_prev[s];
+    const double ex = np >= PP_PREV_KEEP ? in.prev_x[9 * S + s] : in.ego_x[s];
+    const double ey = np >= PP_PREV_KEEP ? in.prev_y[9 * S + s] : in.ego_y[s];
+    const uint64_t order = car_order(in, S, s, ex, ey, iters);
+    sc.order[s] = order;
+    const double* src[4] = {in.car_x, in.car_y, in.car_vx, in.car_vy};
+    double* dst[4] = {sc.x, sc.y, sc.vx, sc.vy};
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+        for (int j = 0; j < iters; j++) col[j * 256 + t] = src[f][(int64_t)j * S + s];
+        for (int k = 0; k < iters; k++) dst[f][(int64_t)k * S + s] = col[(int)((order >> (4 * k)) & 15) * 256 + t];
+    }
+    // the ids in the low half of this lane's own double slots (the waves of the block run without a
+    // barrier: a lane must never touch another lane's slots)
+    int* icol = (int*)col;
+    for (int j = 0; j < iters; j++) icol[2 * (j * 256 + t)] = in.car_id[(int64_t)j * S + s];
+    for (int k = 0; k < iters; k++) sc.id[(int64_t)k * S + s] = icol[2 * ((int)((order >> (4 * k)) & 15) * 256 + t)];
+}
+
+// kK0: k_sort_cars ran (srt holds the rows visit-major); a separate instantiation, so the default
+// path carries no test of it
+template <bool kLdsMap, bool kW4 = false, bool kK0 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : kPrepWaves))) void k_prep(MapG mg, pp_scene_batch in, pp_params P, PrepV pv,
                                               pp_scene_info* info, uint32_t* out_status, GroupBits gb,
-                                              int64_t v0, int64_t v1) {
+                                              int64_t v0, int64_t v1, SortedCars srt) {
     extern __shared__ __attribute__((aligned(16))) double smap[];
     const int n = mg.n;
 #ifdef PP_TRACE
@@ -984,10 +1068,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
     // (v = s D + d), which visit the same rows in lockstep anyway
     uint64_t order = 0xFEDCBA9876543210ull;
     bool sorted = false;
+    // K0 ran (k_sort_cars): its order, and the rows in visit-major arrays
+    constexpr bool k0 = kK0;
+    if (k0) { order = srt.order[s]; sorted = true; }
 #ifdef PP_ABL_NOSORT
     if (false) {
 #else
-    if (!tab && iters > 1 && iters <= 16 && D < PP_SORT_DMAX) {
+    if (!k0 && !tab && iters > 1 && iters <= 16 && D < PP_SORT_DMAX) {
 #endif
         uint32_t key[16];
         bool neg = false;
@@ -1039,9 +1126,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kW4 ? 4 : k
         double cx, cy, cvx, cvy, cs, cd, cvs, cvd;
         int clane = 0;
         if (row >= 0) {
-            const int64_t ix = (int64_t)row * S + s;
-            id = in.car_id[ix];
-            cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
+            if (k0) {                       // visit kk's row, visit-major (coalesced)
+                const int64_t kx = (int64_t)kk * S + s;
+                id = srt.id[kx];
+                cx = srt.x[kx]; cy = srt.y[kx]; cvx = srt.vx[kx]; cvy = srt.vy[kx];
+            } else {
+                const int64_t ix = (int64_t)row * S + s;
+                id = in.car_id[ix];
+                cx = in.car_x[ix]; cy = in.car_y[ix]; cvx = in.car_vx[ix]; cvy = in.car_vy[ix];
+            }
             if (draw > 0) car_noise(P, s, draw, row, cx, cy, cvx, cvy);
             int nwp = 0;
             PP_DIAGC(17, true);
@@ -3258,6 +3351,8 @@ struct StreamWS {
     int64_t rec_cap = 0;
     uint32_t* gbits = nullptr;    // k_cand groups holding a kLimSlow scene (bitmap; all zero between calls)
     int64_t gbits_cap = 0;        // words
+    void* srt = nullptr;          // k_sort_cars' visit-major rows (SortedCars)
+    size_t srt_cap = 0;           // bytes
     hipStream_t st2[kSplitMax - 1] = {};   // the split's other streams (shard-sized batches)
     hipEvent_t fork = nullptr, join[kSplitMax - 1] = {};
 };
@@ -3768,6 +3863,24 @@ int ensure_ws(StreamWS& W, hipStream_t st, int64_t Sv) {
     return PP_OK;
 }
 
+// k_sort_cars' output for S scenes of `rows` rows each (SortedCars over one allocation)
+size_t srt_bytes(int64_t S, int rows) { return (size_t)S * ((size_t)rows * (4 * sizeof(double) + sizeof(int)) + 8) + 256; }
+int ensure_srt(StreamWS& W, hipStream_t st, int64_t S, int rows, SortedCars& sc) {
+    const size_t need = srt_bytes(S, rows);
+    if (W.srt_cap < need) {
+        if (W.srt) { (void)hipStreamSynchronize(st); (void)hipFree(W.srt); W.srt = nullptr; W.srt_cap = 0; }
+        if (hipMalloc(&W.srt, need) != hipSuccess) return PP_ERR_NOMEM;
+        W.srt_cap = need;
+    }
+    double* b = (double*)W.srt;
+    const int64_t n = (int64_t)rows * S;
+    sc.x = b; sc.y = b + n; sc.vx = b + 2 * n; sc.vy = b + 3 * n;
+    sc.id = (int*)(b + 4 * n);
+    sc.order = (uint64_t*)(((uintptr_t)(sc.id + n) + 7) & ~(uintptr_t)7);
+    sc.rows = rows;
+    return PP_OK;
+}
+
 int ensure_rec(StreamWS& W, hipStream_t st, int64_t S) {
     const int64_t cap = (S + 63) & ~(int64_t)63;   // whole 64-scene blocks
     if (W.rec_cap >= cap) return PP_OK;
@@ -3801,6 +3914,7 @@ void free_ws(StreamWS& W) {
     if (W.ws) (void)hipFree(W.ws);
     if (W.rec) (void)hipFree(W.rec);
     if (W.gbits) (void)hipFree(W.gbits);
+    if (W.srt) (void)hipFree(W.srt);
     W = StreamWS();
 }
 
@@ -4139,6 +4253,15 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
     // decision and stores the winner's spline slot in the record's memory (616 B per scene of its
     // 3,088), k_winner_st re-runs the winner from it
     double* wslot = nullptr;
+    // K0 (k_sort_cars) ahead of the one-lane K1: no car table, fewer than PP_SORT_DMAX draws, at
+    // most 16 rows per scene (k_prep's own sorting rule; larger tables keep the identity order)
+    SortedCars srt = {};
+    const int k0f = dbg(PP_DBG_SORT_CARS);
+    if ((k0f == 1 || (k0f == 0 && PP_SORT_K0)) && !in->tab_valid && Dn < PP_SORT_DMAX && in->car_stride >= 2 &&
+        in->car_stride <= 16 && prep_group(Sv) == 1) {
+        rc = ensure_srt(W, st, S, in->car_stride, srt);
+        if (rc) return rc;
+    }
     size_t cand_lds = cg.lds;
     if (PP_WSLOT && !ref_direct && !prm->emit_paths && cg.bps == 1 && Dn == 1) {
         rc = ensure_rec(W, st, S);
@@ -4161,6 +4284,7 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             if (w) return PP_ERR_STATE;
         const bool ok = fill(W.ws, prep_bytes(W.ws_cap)) &&
                         fill(W.rec, W.rec ? rec_bytes(W.rec_cap) : 0) &&
+                        fill(W.srt, W.srt ? W.srt_cap : 0) &&
                         fill(W.gbits + W.gbits_cap + kPartMax, sizeof(uint32_t) * 32 * (size_t)W.gbits_cap) &&
                         fill(out->winner, 4 * S) && fill(out->n_out, 4 * S) && fill(out->status, 4 * S) &&
                         fill(out->next_x, 8 * N * S) && fill(out->next_y, 8 * N * S) &&
@@ -4289,12 +4413,22 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
                 const int eh = 4 * launched++;
                 if (tall) (void)hipEventRecord(ev(eh), sh);
                 const unsigned pb = (unsigned)((v1 - v0 + 255) / 256);
-                if (prep_w4(v1 - v0, device)) {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
-                    else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                if (srt.rows)         // (the split takes batches without draws: scene = evaluation)
+                    hipLaunchKernelGGL(k_sort_cars, dim3(pb), dim3(256), 0, sh, B, srt, v0, v1);
+                if (srt.rows) {
+                    if (prep_w4(v1 - v0, device)) {
+                        if (lmap) hipLaunchKernelGGL((k_prep<true, true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                        else hipLaunchKernelGGL((k_prep<false, true, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                    } else {
+                        if (lmap) hipLaunchKernelGGL((k_prep<true, false, true>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                        else hipLaunchKernelGGL((k_prep<false, false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                    }
+                } else if (prep_w4(v1 - v0, device)) {
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3(pb), dim3(256), lds, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
                 } else {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1);
-                    else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3(pb), dim3(256), lds_a, sh, mga, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3(pb), dim3(256), 0, sh, mg, B, P, pv, R.info, R.status, gbh, v0, v1, srt);
                 }
                 if (tk2) (void)hipEventRecord(ev(eh + 1), sh);
                 const unsigned nsl = (unsigned)std::min<int64_t>(g1 - g0, 2048);
@@ -4338,12 +4472,22 @@ int32_t eval_impl(pp_map* M, const pp_scene_batch* in, const pp_params* prm, pp_
             case 8: { PP_LAUNCH_PREP(k_prep_g8); break; }
             case 16: { PP_LAUNCH_PREP(k_prep_g16); break; }
             default: {
-                if (prep_w4(Sv, device)) {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                if (srt.rows)
+                    hipLaunchKernelGGL(k_sort_cars, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, B, srt, (int64_t)0, S);
+                if (srt.rows) {
+                    if (prep_w4(Sv, device)) {
+                        if (lmap) hipLaunchKernelGGL((k_prep<true, true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                        else hipLaunchKernelGGL((k_prep<false, true, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                    } else {
+                        if (lmap) hipLaunchKernelGGL((k_prep<true, false, true>), dim3((unsigned)blocks), dim3(threads), lds_a, st, mga, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                        else hipLaunchKernelGGL((k_prep<false, false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                    }
+                } else if (prep_w4(Sv, device)) {
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, true>), dim3((unsigned)blocks), dim3(threads), lds, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                    else hipLaunchKernelGGL((k_prep<false, true>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
                 } else {
-                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds_a, st, mga, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
-                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv);
+                    if (lmap) hipLaunchKernelGGL((k_prep<true, false>), dim3((unsigned)blocks), dim3(threads), lds_a, st, mga, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
+                    else hipLaunchKernelGGL((k_prep<false, false>), dim3((unsigned)blocks), dim3(threads), 0, st, mg, B, P, pv, R.info, R.status, gb, (int64_t)0, Sv, srt);
                 }
                 break;
             }
@@ -4414,6 +4558,7 @@ int32_t pp_debug_set(int32_t key, int32_t value) {
         case PP_DBG_SHAPE: ok = value >= 0 && value <= PP_SHAPE_STEP; break;
         case PP_DBG_POISON: ok = value == 0 || value == 1; break;
         case PP_DBG_SPLIT: ok = value >= 0 && value <= 2; break;
+        case PP_DBG_SORT_CARS: ok = value >= 0 && value <= 2; break;
         default: break;       // (PP_DBG_LAST_PARTS is read-only)
     }
     if (!ok) return PP_ERR_ARG;

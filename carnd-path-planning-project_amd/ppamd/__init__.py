@@ -562,7 +562,7 @@ DATA_DIR = os.path.join(os.path.dirname(_HERE), "data")
 TIMING_ALL, TIMING_K2 = 1, 2
 
 # pp_debug_set keys and launch shapes (include/pp.h PP_DBG_*, PP_SHAPE_*)
-DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT, DBG_LAST_PARTS = 0, 1, 2, 3, 4, 5
+DBG_PREP_GROUP, DBG_PREP_WAVES, DBG_SHAPE, DBG_POISON, DBG_SPLIT, DBG_LAST_PARTS, DBG_SORT_CARS = 0, 1, 2, 3, 4, 5, 6
 SPLIT_AUTO, SPLIT_ON, SPLIT_OFF = 0, 1, 2
 SHAPE_AUTO, SHAPE_SPLIT, SHAPE_CAND_SMALL, SHAPE_STEP = 0, 1, 2, 3
 

@@ -390,6 +390,9 @@ int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
  *                      mode without paths or draws, more than 65,536 scenes, at least 2,048), 2 off
  *                      (0: batches of 131,072 scenes and more)
  *   PP_DBG_LAST_PARTS  read-only: the parts the last pp_eval launched, 1 when not split
+ *   PP_DBG_SORT_CARS   1: order each scene's cars in a pre-pass (k_sort_cars) so the one-lane K1
+ *                      reads them visit-major (coalesced; same results, less fetched, slower),
+ *                      2 or 0: K1 sorts and gathers them itself (the default)
  * Returns PP_ERR_ARG for an unknown key or value. */
 #define PP_DBG_PREP_GROUP  0
 #define PP_DBG_PREP_WAVES  1
@@ -397,7 +400,8 @@ int32_t pp_ws_accept_key(const char* key, char* out, int32_t cap);
 #define PP_DBG_POISON      3
 #define PP_DBG_SPLIT       4
 #define PP_DBG_LAST_PARTS  5
-#define PP_DBG_KEYS        6
+#define PP_DBG_SORT_CARS   6
+#define PP_DBG_KEYS        7
 #define PP_SHAPE_SPLIT      1
 #define PP_SHAPE_CAND_SMALL 2
 #define PP_SHAPE_STEP       3

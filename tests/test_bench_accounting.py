@@ -17,7 +17,7 @@ def test_every_pmc_entry_states_its_launch():
     for tag, e in PMC.items():
         assert e["candidates_per_launch"] == e["scenes"] * e["candidates_per_scene"], tag
         assert bench.pmc_tag(e["scenes"], e["candidates_per_scene"], e["n_points"], e["emit_paths"],
-                             e.get("draws", 1)) == tag
+                             e.get("draws", 1), e.get("comfort", False)) == tag
 
 
 @pytest.mark.parametrize("tag", [t for t in PMC if PMC[t]["emit_paths"]])
@@ -81,7 +81,7 @@ def test_rocprof_summary_entries():
         assert lps in (1, 2, 3, 4), tag
         assert e["candidates_per_launch"] == e["scenes"] * e["candidates_per_scene"] // lps, tag
         assert bench.pmc_tag(e["scenes"], e["candidates_per_scene"], e["n_points"], e["emit_paths"],
-                             e.get("draws", 1)) == tag
+                             e.get("draws", 1), e.get("comfort", False)) == tag
         assert 0 < e["dominant_ms_per_launch"] < 100, tag
         bpc = bench.algorithmic_bytes_per_candidate(e["candidates_per_scene"], e["n_points"], e["emit_paths"])
         frac = bpc * e["candidates_per_launch"] / (e["dominant_ms_per_launch"] * 1e-3) / 1e9 / bench.HBM_PEAK_GBS

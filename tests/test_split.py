@@ -73,3 +73,32 @@ def test_forced_split_small_batch_runs_one_stream(env):
     b = run(env, sc, prm, ppamd.SPLIT_OFF, 1)
     for k in a:
         assert (np.asarray(a[k]).view(np.uint8) == np.asarray(b[k]).view(np.uint8)).all(), k
+
+
+@pytest.mark.parametrize("S,draws,mode", [(70013, 0, ppamd.SPLIT_OFF), (140000, 0, ppamd.SPLIT_AUTO),
+                                          (20011, 4, ppamd.SPLIT_OFF)])
+def test_sort_cars_prepass_bit_identical(env, S, draws, mode):
+    """PP_DBG_SORT_CARS 1 (round 6): k_sort_cars orders each scene's cars ahead of the one-lane K1,
+    which then reads them visit-major. The values are copies in k_prep's own visiting order, so
+    every output — the Frenet info, the planner's decision, paths and costs — is the gathering K1's
+    bit for bit: one stream, the two-part split, and Monte-Carlo draws (per-scene order, per-draw
+    noise on the original row). Round 6 measured it: K1's fetch 8.8 -> 3.0 GB per
+    config-5 step, but K0 + K1 0.33 ms slower, so it is off by default."""
+    t = env["torch"]
+    sc = ppamd.synth_host(env["m"], S, seed=S + 7, first=S)
+    idx = np.arange(5, S, 307)
+    sc["ego_speed_mph"][idx] = np.array([-0.0, 5e-324, 3e6, -3.0])[np.arange(len(idx)) % 4]
+    sc["car_id"][3, idx[::3]] = -1                 # the 'no car' sentinel: identity order
+    sc["n_cars"][idx[1::5]] = 1                   # one row: no sort
+    prm = ppamd.default_params(n_draws=draws, cost_mode=ppamd.COST_COMFORT if draws else ppamd.COST_REFERENCE)
+    d = {k: t.from_numpy(np.ascontiguousarray(v)).to(env["dev"]) for k, v in sc.items()}
+    out = {}
+    for k0 in (1, 2):
+        r = ppamd.alloc_result(S, prm, xp="torch", device=env["dev"], info=True)
+        with ppamd.debug(ppamd.DBG_SPLIT, mode), ppamd.debug(ppamd.DBG_SORT_CARS, k0):
+            ppamd.evaluate(env["m"], d, prm, r, device=0)
+        t.cuda.synchronize()
+        out[k0] = ppamd.result_to_numpy(r)
+    for k in out[1]:
+        a, b = np.asarray(out[1][k]), np.asarray(out[2][k])
+        assert (a.view(np.uint8) == b.view(np.uint8)).all(), k
